@@ -1,0 +1,193 @@
+/*
+ * smolcsum.h — C ABI of the MI355X (gfx950) Internet-checksum engine.
+ *
+ * This is the drop-in boundary for the one hot path of smoltcp 0.13.1 that this repository
+ * accelerates: the RFC 1071 one's-complement checksum of `smoltcp::wire::checksum` and the
+ * per-protocol emit/verify gates built on it.  Every entry point below names the reference
+ * interface it replaces (paths relative to the smoltcp source tree).
+ *
+ * Two groups of entry points:
+ *
+ *  1. Scalar host mirrors of `smoltcp::wire::checksum` (src/wire/ip.rs:762-869).  Bit-identical
+ *     results, same argument meaning, host memory, synchronous.  A Rust `extern "C"` binding
+ *      can route `checksum::data` & co. here unchanged.
+ *
+ *  2. Batched device entry points.  One contiguous DEVICE buffer holds many records (IP packets,
+ *     Ethernet frames or raw spans); a record is either described by a descriptor array (device
+ *     memory) or implied by a fixed stride.  Each call is asynchronous and stream-ordered on the
+ *     HIP stream passed in; the caller owns every buffer.  The engine reads the IP header inside
+ *     the record to find the protocol, the L4 span and the pseudo-header addresses, exactly as
+ *     smoltcp's iface does before it calls the per-protocol gates:
+ *       - smol_csum_batch_emit   == the checksum part of Ipv4Repr/UdpRepr/TcpRepr/Icmpv4Repr/
+ *         Icmpv6Repr/IgmpRepr::emit under `caps` (fill when caps.X.tx(), else write 0);
+ *       - smol_csum_batch_verify == the checksum gates of the matching Repr::parse under `caps`
+ *         (verify when caps.X.rx()), reported as one status byte per record;
+ *       - smol_csum_batch_data   == checksum::data() over each raw span.
+ *     A device that offloads checksums (phy::Device with ChecksumCapabilities::ignored(),
+ *     src/phy/mod.rs:223-233) runs emit in TxToken::consume and verify before yielding an
+ *     RxToken, with the stack's default caps (Checksum::Both).
+ *
+ * Errors: every function returning int returns SMOL_OK (0) or a negative SMOL_E* code.  No C++
+ * exception crosses this boundary.  There is no CPU fallback for the batched calls: with no
+ * usable HIP device they return SMOL_ENODEV.
+ *
+ * Threading: a context belongs to one device and one host thread at a time (not thread-safe);
+ * use one context per host thread.  Calls on the same stream are ordered.
+ */
+#ifndef SMOLCSUM_H
+#define SMOLCSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMOLCSUM_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------------------------ */
+enum {
+    SMOL_OK = 0,
+    SMOL_EINVAL = -1,  /* bad argument: NULL pointer with n > 0, unknown kind, bad caps value   */
+    SMOL_ENODEV = -2,  /* no HIP device, or the device ordinal is out of range                   */
+    SMOL_EHIP = -3,    /* a HIP runtime call failed; smol_csum_last_error() gives the message    */
+    SMOL_ERANGE = -4,  /* a size limit was exceeded (record longer than SMOL_MAX_RECORD_LEN)     */
+    SMOL_ENOMEM = -5   /* host allocation failed                                                 */
+};
+
+/* Longest record the batched kernels accept.  Protocol records never exceed 65535 + 14 bytes
+ * (u16 length fields); raw data() spans may be up to 1 GiB.  data() stays bit-exact with the
+ * reference's release-mode u32 wrap-around for spans longer than 131074 bytes (src/wire/ip.rs:776). */
+#define SMOL_MAX_RECORD_LEN (1u << 30)
+
+/* ---- policy: mirrors phy::Checksum / phy::ChecksumCapabilities (src/phy/mod.rs:176-218) --- */
+typedef enum {
+    SMOL_CHECKSUM_BOTH = 0, /* Checksum::Both (the default, src/phy/mod.rs:178) */
+    SMOL_CHECKSUM_RX = 1,   /* Checksum::Rx */
+    SMOL_CHECKSUM_TX = 2,   /* Checksum::Tx */
+    SMOL_CHECKSUM_NONE = 3  /* Checksum::None */
+} smol_checksum_t;
+
+/* Field order and meaning of ChecksumCapabilities {ipv4, udp, tcp, icmpv4, icmpv6}.  Each byte is
+ * a smol_checksum_t.  IGMP has no entry in the reference: IgmpRepr::emit always fills
+ * (src/wire/igmp.rs:293) and IgmpRepr::parse never verifies (src/wire/igmp.rs:204-248); the
+ * batched calls do the same. */
+typedef struct {
+    uint8_t ipv4;
+    uint8_t udp;
+    uint8_t tcp;
+    uint8_t icmpv4;
+    uint8_t icmpv6;
+    uint8_t reserved[3]; /* must be 0 */
+} smol_checksum_caps_t;
+
+/* ---- record kinds ----------------------------------------------------------------------- */
+enum {
+    SMOL_KIND_RAW = 0, /* a plain byte span: only smol_csum_batch_data is meaningful            */
+    SMOL_KIND_IP = 1,  /* an IPv4 or IPv6 packet (Medium::Ip); version from the first nibble     */
+    SMOL_KIND_ETH = 2  /* an Ethernet II frame (Medium::Ethernet) carrying IPv4 (0x0800) or IPv6
+                          (0x86DD); other ethertypes are reported SMOL_ST_UNSUPPORTED           */
+};
+
+/* One record of a batch (16 bytes, device memory).  `len` is the number of bytes the device
+ * buffer holds for this record (the Rx/Tx token buffer length); the IP length fields inside the
+ * record decide the spans that are summed, exactly as in the reference. */
+typedef struct {
+    uint64_t offset; /* byte offset of the record from the batch base pointer (any alignment) */
+    uint32_t len;    /* record length in bytes, <= SMOL_MAX_RECORD_LEN                         */
+    uint8_t kind;    /* SMOL_KIND_*                                                            */
+    uint8_t flags;   /* reserved, must be 0                                                    */
+    uint16_t reserved;
+} smol_csum_desc_t;
+
+/* Batch geometry (host memory).  If `desc` is non-NULL it is a DEVICE array of `n` descriptors
+ * and `stride`/`len`/`kind` are ignored.  Otherwise record i starts at base + i*stride, has
+ * length `len` and kind `kind` (the fixed-size case: no descriptor traffic at all). */
+typedef struct {
+    const smol_csum_desc_t* desc;
+    uint64_t n;
+    uint64_t stride;
+    uint32_t len;
+    uint8_t kind;
+    uint8_t reserved[3];
+} smol_csum_batch_t;
+
+/* ---- per-record status byte (verify; emit reports the MALFORMED/UNSUPPORTED bits) ------- */
+enum {
+    SMOL_ST_IP_OK = 0x01,      /* IPv4 header gate passed: verified under caps.ipv4.rx(), or not
+                                  checked (caps, IPv6, non-IP).  Ipv4Repr::parse, ipv4.rs:553   */
+    SMOL_ST_L4_OK = 0x02,      /* L4 gate passed: verified under caps.X.rx(), or not checked
+                                  (caps, IGMP, fragment, unsupported protocol)                    */
+    SMOL_ST_L4_PARTIAL = 0x04, /* UDP/TCP verify_partial_checksum(): field == pseudo-header sum
+                                  (udp.rs:112-119, tcp.rs:376-385)                              */
+    SMOL_ST_IP_VALID = 0x08,   /* Ipv4Packet::verify_checksum() regardless of caps (1 if no
+                                  IPv4 header)                                                   */
+    SMOL_ST_L4_VALID = 0x10,   /* the L4 verify_checksum() regardless of caps (1 if no L4 span)  */
+    SMOL_ST_MALFORMED = 0x20,  /* a check_len() on the path failed: the reference drops the
+                                  packet before any checksum is looked at                        */
+    SMOL_ST_UNSUPPORTED = 0x40,/* no L4 checksum on this record's path: IPv4 fragment, protocol
+                                  smoltcp does not checksum, IPv6 next header other than a
+                                  leading Hop-by-Hop + TCP/UDP/ICMPv6, non-IP ethertype          */
+    SMOL_ST_ACCEPT = 0x80      /* IP_OK && L4_OK && !MALFORMED: the checksum gates pass         */
+};
+
+/* ---- 1. scalar host mirrors of smoltcp::wire::checksum ---------------------------------- */
+
+/* checksum::data — src/wire/ip.rs:773-804.  RFC 1071 sum without the final complement. */
+uint16_t smol_csum_data(const uint8_t* data, size_t len);
+
+/* checksum::combine — src/wire/ip.rs:807-813. */
+uint16_t smol_csum_combine(const uint16_t* checksums, size_t n);
+
+/* checksum::pseudo_header_v4 — src/wire/ip.rs:816-831.  `length` is truncated to u16 as in the
+ * reference (NetworkEndian::write_u16(.., length as u16)). */
+uint16_t smol_csum_pseudo_header_v4(const uint8_t src_addr[4], const uint8_t dst_addr[4],
+                                    uint8_t next_header, uint32_t length);
+
+/* checksum::pseudo_header_v6 — src/wire/ip.rs:834-849. */
+uint16_t smol_csum_pseudo_header_v6(const uint8_t src_addr[16], const uint8_t dst_addr[16],
+                                    uint8_t next_header, uint32_t length);
+
+/* checksum::pseudo_header — src/wire/ip.rs:851-869.  `family` is 4 or 6 for each address; the
+ * reference panics (unreachable!) on a family mismatch; this returns SMOL_EINVAL instead and
+ * writes nothing. */
+int smol_csum_pseudo_header(int src_family, const uint8_t* src_addr, int dst_family,
+                            const uint8_t* dst_addr, uint8_t next_header, uint32_t length,
+                            uint16_t* out);
+
+/* ---- 2. batched device engine ----------------------------------------------------------- */
+
+typedef struct smol_csum_ctx smol_csum_ctx_t;
+
+/* Create a context bound to HIP device `device`.  Returns SMOL_ENODEV when no such device. */
+int smol_csum_ctx_create(int device, smol_csum_ctx_t** out);
+int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx);
+
+/* checksum::data() over every record span; d_out[i] = data(record i) (u16, numeric value as the
+ * reference returns it).  Record kinds are ignored: every record is a raw span. */
+int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
+                         const smol_csum_batch_t* batch, uint16_t* d_out, void* stream);
+
+/* In-place emit: for every record write the IPv4 header checksum and the L4 checksum the way the
+ * reference's Repr::emit does under `caps` (fill when tx(), else 0; UDP 0 -> 0xffff; IGMP always
+ * filled).  `d_status` (nullable) receives SMOL_ST_MALFORMED / SMOL_ST_UNSUPPORTED per record. */
+int smol_csum_batch_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
+                         const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
+
+/* Verify: d_status[i] = SMOL_ST_* bits for record i under `caps` (Repr::parse gates). */
+int smol_csum_batch_verify(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
+                           const smol_csum_batch_t* batch, const smol_checksum_caps_t* caps,
+                           uint8_t* d_status, void* stream);
+
+/* Message of the last SMOL_EHIP error on this thread ("" if none). */
+const char* smol_csum_last_error(void);
+
+/* ABI version compiled into the library (SMOLCSUM_ABI_VERSION). */
+int smol_csum_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SMOLCSUM_H */

@@ -1,0 +1,149 @@
+"""CPU ORACLE — test infrastructure only.
+
+Two independent restatements of smoltcp 0.13.1's Internet checksum:
+
+* ``pyref`` — pure-Python loops over ``src/wire/ip.rs:762-869`` (small inputs only), used to
+  cross-check the C restatement and to generate golden vectors;
+* ``lib()`` — ctypes handle to ``liboracle.so`` built from ``csum_oracle.c`` (the per-protocol
+  gates and the record/batch contract of ``include/smolcsum.h``).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this package, and only as the checker or the timed CPU baseline.  The product
+(``smoltcp_amd``) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from . import pyref  # noqa: F401
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class CapsC(ctypes.Structure):
+    """smol_checksum_caps_t (include/smolcsum.h)."""
+
+    _fields_ = [
+        ("ipv4", ctypes.c_uint8),
+        ("udp", ctypes.c_uint8),
+        ("tcp", ctypes.c_uint8),
+        ("icmpv4", ctypes.c_uint8),
+        ("icmpv6", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 3),
+    ]
+
+
+def build() -> str:
+    """Compile liboracle.so with the committed Makefile; returns its path."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return os.path.join(_HERE, "liboracle.so")
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = os.path.join(_HERE, "liboracle.so")
+    if not os.path.exists(path):
+        build()
+    L = ctypes.CDLL(path)
+    u8p = ctypes.c_void_p
+    L.oracle_data.argtypes = [u8p, ctypes.c_size_t]
+    L.oracle_data.restype = ctypes.c_uint16
+    L.oracle_combine.argtypes = [u8p, ctypes.c_size_t]
+    L.oracle_combine.restype = ctypes.c_uint16
+    for name in ("oracle_pseudo_v4", "oracle_pseudo_v6"):
+        f = getattr(L, name)
+        f.argtypes = [u8p, u8p, ctypes.c_uint8, ctypes.c_uint32]
+        f.restype = ctypes.c_uint16
+    L.oracle_ipv4_verify.argtypes = [u8p]
+    L.oracle_ipv4_verify.restype = ctypes.c_int
+    L.oracle_ipv4_fill.argtypes = [u8p]
+    L.oracle_ipv4_fill.restype = None
+    for name in ("oracle_udp_verify", "oracle_udp_verify_partial"):
+        f = getattr(L, name)
+        f.argtypes = [u8p, ctypes.c_int, u8p, u8p]
+        f.restype = ctypes.c_int
+    L.oracle_udp_fill.argtypes = [u8p, ctypes.c_int, u8p, u8p]
+    L.oracle_udp_fill.restype = None
+    for name in ("oracle_tcp_verify", "oracle_tcp_verify_partial"):
+        f = getattr(L, name)
+        f.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, u8p, u8p]
+        f.restype = ctypes.c_int
+    L.oracle_tcp_fill.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, u8p, u8p]
+    L.oracle_tcp_fill.restype = None
+    for name in ("oracle_icmpv4_verify", "oracle_igmp_verify"):
+        f = getattr(L, name)
+        f.argtypes = [u8p, ctypes.c_size_t]
+        f.restype = ctypes.c_int
+    for name in ("oracle_icmpv4_fill", "oracle_igmp_fill"):
+        f = getattr(L, name)
+        f.argtypes = [u8p, ctypes.c_size_t]
+        f.restype = None
+    L.oracle_icmpv6_verify.argtypes = [u8p, ctypes.c_size_t, u8p, u8p]
+    L.oracle_icmpv6_verify.restype = ctypes.c_int
+    L.oracle_icmpv6_fill.argtypes = [u8p, ctypes.c_size_t, u8p, u8p]
+    L.oracle_icmpv6_fill.restype = None
+    L.oracle_record_verify.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(CapsC)]
+    L.oracle_record_verify.restype = ctypes.c_uint8
+    L.oracle_record_emit.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(CapsC)]
+    L.oracle_record_emit.restype = ctypes.c_uint8
+    L.oracle_batch_data.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, u8p]
+    L.oracle_batch_data.restype = None
+    L.oracle_batch_emit.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                    ctypes.c_uint8, ctypes.POINTER(CapsC), u8p]
+    L.oracle_batch_emit.restype = None
+    L.oracle_batch_verify.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.c_uint8, ctypes.POINTER(CapsC), u8p]
+    L.oracle_batch_verify.restype = None
+    _LIB = L
+    return L
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def caps_c(caps=(0, 0, 0, 0, 0)) -> CapsC:
+    c = CapsC()
+    c.ipv4, c.udp, c.tcp, c.icmpv4, c.icmpv6 = (int(x) for x in caps)
+    return c
+
+
+# ---- thin numpy wrappers ------------------------------------------------------------------
+
+
+def data(b) -> int:
+    a = np.frombuffer(bytes(b), dtype=np.uint8)
+    return int(lib().oracle_data(_ptr(a) if a.size else None, a.size))
+
+
+def batch_data(buf: np.ndarray, desc: np.ndarray | None, n: int, stride: int = 0, length: int = 0):
+    out = np.zeros(n, dtype=np.uint16)
+    lib().oracle_batch_data(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride, length,
+                            _ptr(out))
+    return out
+
+
+def batch_emit(buf: np.ndarray, desc, n: int, stride: int = 0, length: int = 0, kind: int = 1,
+               caps=(0, 0, 0, 0, 0)):
+    """In place on ``buf`` (host numpy uint8); returns the status array."""
+    st = np.zeros(n, dtype=np.uint8)
+    c = caps_c(caps)
+    lib().oracle_batch_emit(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride, length,
+                            kind, ctypes.byref(c), _ptr(st))
+    return st
+
+
+def batch_verify(buf: np.ndarray, desc, n: int, stride: int = 0, length: int = 0, kind: int = 1,
+                 caps=(0, 0, 0, 0, 0)):
+    st = np.zeros(n, dtype=np.uint8)
+    c = caps_c(caps)
+    lib().oracle_batch_verify(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride,
+                              length, kind, ctypes.byref(c), _ptr(st))
+    return st
