@@ -1,0 +1,291 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident batched Internet checksum (emit + verify) on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): per GPU 2^20 IPv4/UDP datagrams of 1500 bytes in HBM
+at a fixed 1500-byte stride.  One step = smol_csum_batch_emit over the TX batch (fill the IPv4
+header and UDP checksums) + smol_csum_batch_verify over the RX batch (the same kind of datagrams,
+already emitted, with 1/64 of them single-bit corrupted as phy::FaultInjector does).  Metric: GiB/s
+checksummed = bytes covered by checksum::data spans (IPv4 header + UDP length) of both passes ÷
+wall time, summed over GPUs (weak scaling: every rank owns its own batch; no collective on the
+data path — only barrier + a max-reduction of the elapsed time for reporting).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (see the contract in the task description / DESIGN.md §Measurement).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s checksummed (device-resident), batched 1500B segments, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+GIB = float(1 << 30)
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--n", type=int, default=0, help="records per GPU (default: the config's)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (0: skip)")
+    ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
+    ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------------------------
+# Workloads
+# ---------------------------------------------------------------------------------------------
+
+
+class Workload:
+    """Two HBM batches (tx, rx) of one config, generated on the device."""
+
+    def __init__(self, E, eng, cfg: str, n: int, rank: int, dev):
+        import torch
+
+        self.cfg = cfg
+        self.E = E
+        seed = {"c2": 0x5EED0001, "c3": 0x5EED0002, "c4": 0x5EED0003, "c5": 0x5EED0005}[cfg] + 1000 * rank
+        self.seed = seed
+        if cfg in ("c2", "c5"):
+            self.n = n or (1 << 20 if cfg == "c2" else 128 << 20)
+            L = 1500
+            self.kind, self.profile = E.KIND_IP, E.SYNTH_UDP4
+            self.batch = E.Batch.fixed(self.n, L, L, E.KIND_IP)
+            self.total = self.n * L
+            self.span_bytes = self.n * 1500  # IPv4 header (20) + UDP length (1480)
+            self.read_bytes = self.n * L
+            self.desc_bytes = 0
+            self.workload = (f"C2: {self.n} x 1500 B IPv4/UDP datagrams, fixed stride, emit (tx) + "
+                             f"verify (rx, 1/64 single-bit corrupted)") if cfg == "c2" else \
+                (f"C5: {self.n} x 1500 B IPv4/UDP per GPU, in-place emit + verify of one batch")
+        elif cfg == "c3":
+            self.n = n or (1 << 20)
+            rng = np.random.default_rng(seed)
+            lens = rng.integers(64, 9001, self.n).astype(np.uint32)
+            offs = np.zeros(self.n, dtype=np.uint64)
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+            self.kind, self.profile = E.KIND_IP, E.SYNTH_TCP4
+            self.batch = E.Batch.from_records(offs, lens, E.KIND_IP, dev)
+            self.total = int(offs[-1] + lens[-1]) + 16
+            self.span_bytes = int(lens.astype(np.uint64).sum())  # header + TCP segment = whole record
+            self.read_bytes = self.span_bytes
+            self.desc_bytes = 16 * self.n
+            self.workload = f"C3: {self.n} IPv4/TCP segments, length U[64,9000], packed (odd offsets) + descriptors"
+        else:  # c4
+            self.n = n or (1 << 20)
+            L = 1320
+            self.kind, self.profile = E.KIND_IP, E.SYNTH_V6MIX
+            self.batch = E.Batch.fixed(self.n, L, L, E.KIND_IP)
+            self.total = self.n * L
+            self.span_bytes = self.n * 1280  # L4 only (IPv6 has no header checksum)
+            self.read_bytes = self.n * L
+            self.desc_bytes = 0
+            self.workload = f"C4: {self.n} IPv6 packets (40 B header + 1280 B TCP/UDP/ICMPv6 round-robin)"
+        self.tx = torch.empty(self.total, dtype=torch.uint8, device=dev)
+        eng.synth(self.tx, self.batch, self.profile, seed)
+        if cfg == "c5":
+            self.rx = self.tx
+        else:
+            self.rx = torch.empty(self.total, dtype=torch.uint8, device=dev)
+            eng.synth(self.rx, self.batch, self.profile, seed ^ 0xABCDEF)
+            eng.emit(self.rx, self.batch)
+            eng.corrupt(self.rx, self.batch, every=64, seed=seed)
+        self.status = torch.empty(self.n, dtype=torch.uint8, device=dev)
+        self.est = None
+
+
+def cpu_baseline(E, wl, seconds: float):
+    """The oracle (a C restatement of smoltcp's scalar checksum + gates, 1 thread) over a bounded
+    sample of the same workload, timed on this host."""
+    import oracle
+
+    if seconds <= 0:
+        return None
+    if wl.batch.desc is None:
+        L = wl.batch.length
+        m = min(wl.n, 32768)
+        tx = wl.tx[: m * L].cpu().numpy().copy()
+        rx = wl.rx[: m * L].cpu().numpy().copy()
+        desc = None
+        stride = L
+        span = wl.span_bytes * m // wl.n
+    else:
+        m = min(wl.n, 8192)
+        d = wl.batch.desc[: 16 * m].cpu().numpy().view(E.DESC_DTYPE).copy()
+        end = int(d["offset"][-1] + d["len"][-1])
+        tx = wl.tx[:end].cpu().numpy().copy()
+        rx = wl.rx[:end].cpu().numpy().copy()
+        desc, stride, L = d, 0, 0
+        span = int(d["len"].astype(np.uint64).sum())
+    caps = (0, 0, 0, 0, 0)
+    oracle.lib()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.batch_emit(tx, desc, m, stride, L, wl.kind, caps)
+        oracle.batch_verify(rx, desc, m, stride, L, wl.kind, caps)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gibs = 2 * span * reps / el / GIB
+    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{m} records of the same workload (emit tx + verify rx), {reps} passes in {el:.1f} s, "
+                      f"oracle/csum_oracle.c (gcc -O3 -march=x86-64-v3), 1 thread"}
+
+
+def load_traffic(cfg: str, kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/*traffic*.json)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except Exception:
+            continue
+        ent = t.get(cfg, {}).get(kernel)
+        if ent and "hbm_bytes_per_launch" in ent:
+            return ent["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    from smoltcp_amd import engine as E
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    eng = E.ChecksumEngine(local)
+    if args.shape >= 0:
+        eng.set_shape(args.shape)
+    wl = Workload(E, eng, args.config, args.n, rank, dev)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        eng.emit(wl.tx, wl.batch, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        eng.verify(wl.rx, wl.batch, status=wl.status, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-kernel HIP events on the launch stream, every step of the timed region
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    emit_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    verify_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+
+    # correctness of the last verify against the oracle on a sample (and the expected rejections)
+    st = wl.status.cpu().numpy()
+    rejected = int(((st & E.ST_ACCEPT) == 0).sum())
+
+    probe = None
+    if args.probe and rank == 0:
+        sink = torch.zeros(1, dtype=torch.int32, device=dev)
+        for _ in range(3):
+            eng.stream_read(wl.rx, sink)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(10):
+            eng.stream_read(wl.rx, sink, stream=stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / 10
+        probe = {"kernel": "stream_read_kernel", "bytes": wl.rx.numel() // 16 * 16, "ms": round(ms, 4),
+                 "GB/s": round(wl.rx.numel() / ms / 1e6, 1)}
+
+    cpu = None
+    if rank == 0 and world == 1:
+        cpu = cpu_baseline(E, wl, args.cpu_seconds)
+
+    if rank == 0:
+        per_step_bytes = 2 * wl.span_bytes * world
+        value = per_step_bytes * args.steps / elapsed / GIB
+        # roofline of the dominant kernel: algorithmic bytes per launch / its mean launch time
+        kernels = {
+            "emit": {"ms": emit_ms, "bytes": wl.read_bytes + wl.desc_bytes + 4 * wl.n},
+            "verify": {"ms": verify_ms, "bytes": wl.read_bytes + wl.desc_bytes + wl.n},
+        }
+        dom = max(kernels, key=lambda k: kernels[k]["ms"])
+        kd = kernels[dom]
+        achieved = kd["bytes"] / (kd["ms"] * 1e-3) / 1e9
+        traffic, tsrc = load_traffic(args.config, dom)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: device-generated packets (splitmix64 payload, seeded), HBM-resident",
+            "config": {"workload": wl.workload, "records_per_gpu": wl.n, "parallelism": f"shard x{world} (no collective)",
+                       "checksummed_bytes_per_step_per_gpu": 2 * wl.span_bytes},
+            "roofline": {"bound": "hbm", "kernel": f"csum_kernel ({dom})", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_source": tsrc,
+                         "algorithmic_bytes_per_launch": kd["bytes"], "launch_ms": round(kd["ms"], 4)},
+            "kernels_ms": {k: round(v["ms"], 4) for k, v in kernels.items()},
+            "verify_rejected": rejected,
+            "cpu_baseline": cpu,
+        }
+        if probe:
+            out["stream_read_probe"] = probe
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,55 @@
+/*
+ * smolcsum_tools.h — benchmark / test tooling exported by libsmolcsum.so.  NOT part of the
+ * drop-in boundary (that is include/smolcsum.h): synthetic packet batches generated on the
+ * device (the 8 x 128 M x 1500 B configuration needs ~190 GB per GPU, which only the device can
+ * produce in reasonable time), single-bit fault injection following phy::FaultInjector's recipe
+ * (src/phy/fault_injector.rs:8-16,45-51), and a launch-shape override for tuning.
+ */
+#ifndef SMOLCSUM_TOOLS_H
+#define SMOLCSUM_TOOLS_H
+
+#include "smolcsum.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    SMOL_SYNTH_UDP4 = 0,     /* IPv4 (IHL 5, DF, TTL 64) + UDP (length = record - 20) + payload */
+    SMOL_SYNTH_TCP4 = 1,     /* IPv4 + TCP (20-byte header, ACK|PSH) + payload                  */
+    SMOL_SYNTH_V6MIX = 2,    /* IPv6 + TCP / UDP / ICMPv6 echo, round-robin by record index     */
+    SMOL_SYNTH_ETH_TCP4 = 3, /* Ethernet II + IPv4 + TCP (Medium::Ethernet frames)              */
+    SMOL_SYNTH_RANDOM = 4    /* random bytes only                                               */
+};
+
+/* Fill every record of `batch` (device buffer) with a synthetic packet of the given profile;
+ * all checksum fields are written as 0 (what Repr::emit writes when the device offloads).
+ * Payload bytes are splitmix64(seed, position).  Deterministic for a given (batch, seed). */
+int smol_csum_tool_synth(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
+                         int profile, uint64_t seed, void* stream);
+
+/* Flip one bit in every `every`-th record (records i with i % every == 0), at a byte index and
+ * bit drawn from xorshift32 seeded by (seed, i) — FaultInjector::corrupt's recipe. */
+int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
+                           uint32_t every, uint64_t seed, void* stream);
+
+/* Force a launch shape for the next batched calls on this context (-1 = automatic).
+ * 0: 16 lanes x 2 chunks, 1: 32 x 3, 2: 64 x 2, 3: 64 x 4 per record step. */
+int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
+
+/* Cap the number of workgroups per launch (0 = automatic: CUs x 8). */
+int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
+
+/* Read-only HBM streaming probe over `bytes` (multiple of 16, 16-byte aligned `d_buf`): the
+ * achievable read ceiling that the checksum kernels are compared with.  `d_sink` is one u32. */
+int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint64_t bytes,
+                               uint32_t* d_sink, void* stream);
+
+/* The launch shape the library picks for an implicit batch of `len`-byte records. */
+int smol_csum_tool_auto_shape(uint32_t len, int has_desc);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SMOLCSUM_TOOLS_H */

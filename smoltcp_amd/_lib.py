@@ -1,0 +1,128 @@
+"""ctypes binding of libsmolcsum.so (the C ABI declared in include/smolcsum.h).
+
+The shared library is built in-tree (``smoltcp_amd/libsmolcsum.so``, see ``__graft_entry__.build``)
+and travels with the repository snapshot to the GPU box.  There is no fallback: if the library is
+missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsmolcsum.so")
+
+SMOL_OK, SMOL_EINVAL, SMOL_ENODEV, SMOL_EHIP, SMOL_ERANGE, SMOL_ENOMEM = 0, -1, -2, -3, -4, -5
+ERROR_NAMES = {
+    SMOL_EINVAL: "SMOL_EINVAL",
+    SMOL_ENODEV: "SMOL_ENODEV",
+    SMOL_EHIP: "SMOL_EHIP",
+    SMOL_ERANGE: "SMOL_ERANGE",
+    SMOL_ENOMEM: "SMOL_ENOMEM",
+}
+
+# Every symbol include/smolcsum.h and include/smolcsum_tools.h declare.
+ABI_SYMBOLS = [
+    "smol_csum_data", "smol_csum_combine", "smol_csum_pseudo_header_v4",
+    "smol_csum_pseudo_header_v6", "smol_csum_pseudo_header", "smol_csum_ctx_create",
+    "smol_csum_ctx_destroy", "smol_csum_batch_data", "smol_csum_batch_emit",
+    "smol_csum_batch_verify", "smol_csum_last_error", "smol_csum_abi_version",
+]
+TOOL_SYMBOLS = [
+    "smol_csum_tool_synth", "smol_csum_tool_corrupt", "smol_csum_tool_set_shape",
+    "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
+]
+
+
+class SmolError(RuntimeError):
+    def __init__(self, rc: int, what: str, detail: str = ""):
+        name = ERROR_NAMES.get(rc, str(rc))
+        super().__init__(f"{what} failed: {name}" + (f" ({detail})" if detail else ""))
+        self.rc = rc
+
+
+class Caps(ctypes.Structure):
+    """smol_checksum_caps_t — phy::ChecksumCapabilities {ipv4, udp, tcp, icmpv4, icmpv6}."""
+
+    _fields_ = [
+        ("ipv4", ctypes.c_uint8),
+        ("udp", ctypes.c_uint8),
+        ("tcp", ctypes.c_uint8),
+        ("icmpv4", ctypes.c_uint8),
+        ("icmpv6", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 3),
+    ]
+
+
+class BatchC(ctypes.Structure):
+    """smol_csum_batch_t."""
+
+    _fields_ = [
+        ("desc", ctypes.c_void_p),
+        ("n", ctypes.c_uint64),
+        ("stride", ctypes.c_uint64),
+        ("len", ctypes.c_uint32),
+        ("kind", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 3),
+    ]
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsmolcsum.so (raises if it is absent: there is no CPU fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u8, u16, u32, u64 = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64
+    sz, i32 = ctypes.c_size_t, ctypes.c_int
+    L.smol_csum_data.argtypes = [vp, sz]
+    L.smol_csum_data.restype = u16
+    L.smol_csum_combine.argtypes = [vp, sz]
+    L.smol_csum_combine.restype = u16
+    L.smol_csum_pseudo_header_v4.argtypes = [vp, vp, u8, u32]
+    L.smol_csum_pseudo_header_v4.restype = u16
+    L.smol_csum_pseudo_header_v6.argtypes = [vp, vp, u8, u32]
+    L.smol_csum_pseudo_header_v6.restype = u16
+    L.smol_csum_pseudo_header.argtypes = [i32, vp, i32, vp, u8, u32, ctypes.POINTER(u16)]
+    L.smol_csum_pseudo_header.restype = i32
+    L.smol_csum_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
+    L.smol_csum_ctx_create.restype = i32
+    L.smol_csum_ctx_destroy.argtypes = [vp]
+    L.smol_csum_ctx_destroy.restype = i32
+    L.smol_csum_batch_data.argtypes = [vp, vp, ctypes.POINTER(BatchC), vp, vp]
+    L.smol_csum_batch_data.restype = i32
+    L.smol_csum_batch_emit.argtypes = [vp, vp, ctypes.POINTER(BatchC), ctypes.POINTER(Caps), vp, vp]
+    L.smol_csum_batch_emit.restype = i32
+    L.smol_csum_batch_verify.argtypes = [vp, vp, ctypes.POINTER(BatchC), ctypes.POINTER(Caps), vp, vp]
+    L.smol_csum_batch_verify.restype = i32
+    L.smol_csum_last_error.argtypes = []
+    L.smol_csum_last_error.restype = ctypes.c_char_p
+    L.smol_csum_abi_version.argtypes = []
+    L.smol_csum_abi_version.restype = i32
+    L.smol_csum_tool_synth.argtypes = [vp, vp, ctypes.POINTER(BatchC), i32, u64, vp]
+    L.smol_csum_tool_synth.restype = i32
+    L.smol_csum_tool_corrupt.argtypes = [vp, vp, ctypes.POINTER(BatchC), u32, u64, vp]
+    L.smol_csum_tool_corrupt.restype = i32
+    L.smol_csum_tool_set_shape.argtypes = [vp, i32]
+    L.smol_csum_tool_set_shape.restype = i32
+    L.smol_csum_tool_set_max_blocks.argtypes = [vp, u32]
+    L.smol_csum_tool_set_max_blocks.restype = i32
+    L.smol_csum_tool_stream_read.argtypes = [vp, vp, u64, vp, vp]
+    L.smol_csum_tool_stream_read.restype = i32
+    L.smol_csum_tool_auto_shape.argtypes = [u32, i32]
+    L.smol_csum_tool_auto_shape.restype = i32
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SMOL_OK:
+        detail = lib().smol_csum_last_error().decode(errors="replace") if rc == SMOL_EHIP else ""
+        raise SmolError(rc, what, detail)

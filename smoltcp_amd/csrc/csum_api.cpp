@@ -1,0 +1,277 @@
+// C ABI of the checksum engine: scalar host mirrors of smoltcp::wire::checksum and the batched
+// device entry points (include/smolcsum.h), plus the tooling entry points
+// (include/smolcsum_tools.h).  No exception crosses this boundary; every batched call either
+// launches HIP kernels or returns an error — there is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/smolcsum.h"
+#include "../../include/smolcsum_tools.h"
+#include "csum_launch.h"
+
+using namespace smolcsum;
+
+struct smol_csum_ctx {
+    int device;
+    int num_cu;
+    uint32_t max_blocks;  // persistent-grid cap (CUs x 8 by default)
+    int shape;            // -1 automatic, else CFG_*
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int hip_fail(hipError_t e, const char* what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return SMOL_EHIP;
+}
+
+struct DeviceGuard {  // run on ctx->device, restore the caller's current device afterwards
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int now = -1;
+        if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
+    }
+};
+
+inline uint16_t fold_u32(uint32_t w) {  // propagate_carries, src/wire/ip.rs:767-770
+    uint32_t s = (w >> 16) + (w & 0xffffu);
+    return (uint16_t)(((s >> 16) + s) & 0xffffu);
+}
+
+inline uint16_t swap16(uint16_t v) { return (uint16_t)((v >> 8) | (v << 8)); }
+
+bool caps_valid(const smol_checksum_caps_t* c) {
+    if (!c) return false;
+    const uint8_t v[5] = {c->ipv4, c->udp, c->tcp, c->icmpv4, c->icmpv6};
+    for (uint8_t x : v)
+        if (x > SMOL_CHECKSUM_NONE) return false;
+    return c->reserved[0] == 0 && c->reserved[1] == 0 && c->reserved[2] == 0;
+}
+
+int auto_shape(uint32_t len, bool has_desc) {
+    if (has_desc) return CFG_G64U4;
+    const uint64_t need = (uint64_t)len + 15;  // bytes of aligned chunks a record can touch
+    if (need <= 16 * 16 * 2) return CFG_G16U2;
+    if (need <= 16 * 32 * 3) return CFG_G32U3;
+    if (need <= 16 * 64 * 2) return CFG_G64U2;
+    return CFG_G64U4;
+}
+
+int check_batch(const smol_csum_batch_t* b, const void* d_buf) {
+    if (!b) return SMOL_EINVAL;
+    if (b->n == 0) return SMOL_OK;
+    if (!d_buf) return SMOL_EINVAL;
+    if (b->desc) {
+        if (((uintptr_t)b->desc & 15u) != 0) return SMOL_EINVAL;
+    } else if (b->len > SMOL_MAX_RECORD_LEN) {
+        return SMOL_ERANGE;
+    }
+    return SMOL_OK;
+}
+
+int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t* b,
+        const smol_checksum_caps_t* caps, uint16_t* d_out, uint8_t* d_status, void* stream) {
+    KParams p;
+    std::memset(&p, 0, sizeof p);
+    p.buf = d_buf;
+    p.desc = b->desc;
+    p.n = b->n;
+    p.stride = b->stride;
+    p.len = b->len;
+    p.kind = b->kind;
+    if (caps) {
+        p.caps_ipv4 = caps->ipv4;
+        p.caps_udp = caps->udp;
+        p.caps_tcp = caps->tcp;
+        p.caps_icmpv4 = caps->icmpv4;
+        p.caps_icmpv6 = caps->icmpv6;
+    }
+    p.out16 = d_out;
+    p.status = d_status;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    const int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr);
+    hipError_t e = launch_csum(mode, shape, p, ctx->max_blocks, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
+    return SMOL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- scalar host mirrors --------------------------------------------------------------------
+
+// checksum::data, src/wire/ip.rs:773-804.  Little-endian u16 words are summed exactly in 64 bits
+// and truncated to 32 bits, which equals the reference's wrapping u32 accumulator.
+uint16_t smol_csum_data(const uint8_t* d, size_t n) {
+    uint64_t acc = 0;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t q;
+        std::memcpy(&q, d + i, 8);
+        acc += (q & 0xffffu) + ((q >> 16) & 0xffffu) + ((q >> 32) & 0xffffu) + (q >> 48);
+    }
+    for (; i + 2 <= n; i += 2) acc += (uint32_t)d[i] | ((uint32_t)d[i + 1] << 8);
+    if (i < n) acc += d[i];
+    return swap16(fold_u32((uint32_t)acc));
+}
+
+// checksum::combine, src/wire/ip.rs:807-813
+uint16_t smol_csum_combine(const uint16_t* c, size_t n) {
+    uint32_t acc = 0;
+    for (size_t i = 0; i < n; i++) acc += c[i];
+    return fold_u32(acc);
+}
+
+static uint16_t pseudo(const uint8_t* src, const uint8_t* dst, size_t alen, uint8_t nh,
+                       uint32_t length) {
+    const uint8_t pl[4] = {0, nh, (uint8_t)(length >> 8), (uint8_t)length};
+    const uint16_t parts[3] = {smol_csum_data(src, alen), smol_csum_data(dst, alen),
+                               smol_csum_data(pl, 4)};
+    return smol_csum_combine(parts, 3);
+}
+
+// checksum::pseudo_header_v4, src/wire/ip.rs:816-831
+uint16_t smol_csum_pseudo_header_v4(const uint8_t src[4], const uint8_t dst[4], uint8_t nh,
+                                    uint32_t length) {
+    return pseudo(src, dst, 4, nh, length);
+}
+
+// checksum::pseudo_header_v6, src/wire/ip.rs:834-849
+uint16_t smol_csum_pseudo_header_v6(const uint8_t src[16], const uint8_t dst[16], uint8_t nh,
+                                    uint32_t length) {
+    return pseudo(src, dst, 16, nh, length);
+}
+
+// checksum::pseudo_header, src/wire/ip.rs:851-869
+int smol_csum_pseudo_header(int src_family, const uint8_t* src, int dst_family,
+                            const uint8_t* dst, uint8_t nh, uint32_t length, uint16_t* out) {
+    if (!src || !dst || !out || src_family != dst_family) return SMOL_EINVAL;
+    if (src_family == 4) { *out = smol_csum_pseudo_header_v4(src, dst, nh, length); return SMOL_OK; }
+    if (src_family == 6) { *out = smol_csum_pseudo_header_v6(src, dst, nh, length); return SMOL_OK; }
+    return SMOL_EINVAL;
+}
+
+// ---- context ---------------------------------------------------------------------------------
+
+int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
+    if (!out) return SMOL_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        g_last_error = "no HIP device";
+        return SMOL_ENODEV;
+    }
+    if (device < 0 || device >= count) return SMOL_ENODEV;
+    int cus = 0;
+    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
+    auto* c = new (std::nothrow) smol_csum_ctx;
+    if (!c) return SMOL_ENOMEM;
+    c->device = device;
+    c->num_cu = cus;
+    c->max_blocks = (uint32_t)(cus > 0 ? cus : 256) * 8u;
+    c->shape = -1;
+    *out = c;
+    return SMOL_OK;
+}
+
+int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
+    delete ctx;
+    return SMOL_OK;
+}
+
+// ---- batched device entry points -------------------------------------------------------------
+
+int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf, const smol_csum_batch_t* b,
+                         uint16_t* d_out, void* stream) {
+    if (!ctx) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK || b->n == 0) return rc;
+    if (!d_out) return SMOL_EINVAL;
+    return run(ctx, MODE_DATA, const_cast<uint8_t*>(d_buf), b, nullptr, d_out, nullptr, stream);
+}
+
+int smol_csum_batch_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* b,
+                         const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream) {
+    if (!ctx || !caps_valid(caps)) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK || b->n == 0) return rc;
+    return run(ctx, MODE_EMIT, d_buf, b, caps, nullptr, d_status, stream);
+}
+
+int smol_csum_batch_verify(smol_csum_ctx_t* ctx, const uint8_t* d_buf, const smol_csum_batch_t* b,
+                           const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream) {
+    if (!ctx || !caps_valid(caps)) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK || b->n == 0) return rc;
+    if (!d_status) return SMOL_EINVAL;
+    return run(ctx, MODE_VERIFY, const_cast<uint8_t*>(d_buf), b, caps, nullptr, d_status, stream);
+}
+
+const char* smol_csum_last_error(void) { return g_last_error.c_str(); }
+
+int smol_csum_abi_version(void) { return SMOLCSUM_ABI_VERSION; }
+
+// ---- tooling (include/smolcsum_tools.h) -------------------------------------------------------
+
+int smol_csum_tool_synth(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* b,
+                         int profile, uint64_t seed, void* stream) {
+    if (!ctx || profile < 0 || profile > SMOL_SYNTH_RANDOM) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK || b->n == 0) return rc;
+    SynthParams p{d_buf, b->desc, b->n, b->stride, b->len, (uint32_t)profile, seed};
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    hipError_t e = launch_synth(p, ctx->max_blocks, (hipStream_t)stream);
+    return e == hipSuccess ? SMOL_OK : hip_fail(e, "synth kernel launch");
+}
+
+int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* b,
+                           uint32_t every, uint64_t seed, void* stream) {
+    if (!ctx || every == 0) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK || b->n == 0) return rc;
+    SynthParams p{d_buf, b->desc, b->n, b->stride, b->len, 0u, seed};
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    hipError_t e = launch_corrupt(p, every, (hipStream_t)stream);
+    return e == hipSuccess ? SMOL_OK : hip_fail(e, "corrupt kernel launch");
+}
+
+int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
+    if (!ctx || shape < -1 || shape >= CFG_COUNT) return SMOL_EINVAL;
+    ctx->shape = shape;
+    return SMOL_OK;
+}
+
+int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks) {
+    if (!ctx) return SMOL_EINVAL;
+    ctx->max_blocks = max_blocks ? max_blocks : (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * 8u;
+    return SMOL_OK;
+}
+
+int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint64_t bytes,
+                               uint32_t* d_sink, void* stream) {
+    if (!ctx || !d_buf || !d_sink || (bytes & 15u) || ((uintptr_t)d_buf & 15u)) return SMOL_EINVAL;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    hipError_t e = launch_stream_read(d_buf, bytes, d_sink, ctx->max_blocks, (hipStream_t)stream);
+    return e == hipSuccess ? SMOL_OK : hip_fail(e, "stream-read kernel launch");
+}
+
+int smol_csum_tool_auto_shape(uint32_t len, int has_desc) { return auto_shape(len, has_desc != 0); }
+
+}  // extern "C"

@@ -1,0 +1,46 @@
+// Host <-> kernel interface of the checksum engine (internal; the public ABI is
+// include/smolcsum.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/smolcsum.h"
+
+namespace smolcsum {
+
+enum { MODE_DATA = 0, MODE_EMIT = 1, MODE_VERIFY = 2 };
+
+// Launch shapes: lanes per record (G) x 16-byte chunks per lane per step (U).
+enum { CFG_G16U2 = 0, CFG_G32U3 = 1, CFG_G64U2 = 2, CFG_G64U4 = 3, CFG_COUNT = 4 };
+
+struct KParams {
+    uint8_t* buf;
+    const smol_csum_desc_t* desc;  // nullptr: implicit fixed-stride batch
+    uint64_t n;
+    uint64_t stride;
+    uint32_t len;
+    uint32_t kind;
+    uint32_t caps_ipv4, caps_udp, caps_tcp, caps_icmpv4, caps_icmpv6;
+    uint16_t* out16;  // MODE_DATA
+    uint8_t* status;  // MODE_VERIFY (required), MODE_EMIT (optional)
+};
+
+hipError_t launch_csum(int mode, int cfg, const KParams& p, uint32_t max_blocks, hipStream_t s);
+
+// Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
+struct SynthParams {
+    uint8_t* buf;
+    const smol_csum_desc_t* desc;
+    uint64_t n;
+    uint64_t stride;
+    uint32_t len;
+    uint32_t profile;
+    uint64_t seed;
+};
+hipError_t launch_synth(const SynthParams& p, uint32_t max_blocks, hipStream_t s);
+hipError_t launch_corrupt(const SynthParams& p, uint32_t every, hipStream_t s);
+hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t max_blocks,
+                              hipStream_t s);
+
+}  // namespace smolcsum

@@ -1,0 +1,231 @@
+// Synthetic packet batches and single-bit fault injection, generated on the device
+// (tooling for tests and bench.py; see include/smolcsum_tools.h).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/smolcsum_tools.h"
+#include "csum_launch.h"
+
+namespace smolcsum {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ uint64_t rnd(uint64_t seed, uint64_t i, uint64_t k) {
+    return splitmix64(seed * 0x100000001B3ull ^ (i * 0x9E3779B97F4A7C15ull) ^ (k << 56));
+}
+
+__device__ __forceinline__ int be16_byte(uint32_t v, uint32_t o) {  // o = 0 (hi) / 1 (lo)
+    return (int)((o == 0 ? (v >> 8) : v) & 0xffu);
+}
+
+// Header byte of an IPv4 + (UDP|TCP) packet of total length L at offset o (relative to the
+// IPv4 header), or -1 past the header.
+__device__ int ipv4_l4_byte(uint32_t proto, uint64_t seed, uint64_t i, uint32_t L, uint32_t o) {
+    if (o < 20) {
+        switch (o) {
+            case 0: return 0x45;
+            case 1: return 0;
+            case 2: case 3: return be16_byte(L, o - 2);
+            case 4: case 5: return be16_byte((uint32_t)(i & 0xffff), o - 4);
+            case 6: return 0x40;  // DF
+            case 7: return 0;
+            case 8: return 64;
+            case 9: return (int)proto;
+            case 10: case 11: return 0;
+            default: {
+                const uint64_t a = rnd(seed, i, 1);
+                return (int)((a >> (8 * (o - 12))) & 0xff);  // src 12..15, dst 16..19
+            }
+        }
+    }
+    const uint32_t t = o - 20;
+    const uint64_t pr = rnd(seed, i, 3);
+    if (proto == 17) {
+        if (t < 8) {
+            switch (t) {
+                case 0: case 1: return be16_byte((uint32_t)(pr & 0xffff), t);
+                case 2: case 3: return be16_byte((uint32_t)((pr >> 16) & 0xffff) | 1u, t - 2);
+                case 4: case 5: return be16_byte(L - 20, t - 4);
+                default: return 0;
+            }
+        }
+        return -1;
+    }
+    if (t < 20) {  // TCP
+        if (t < 4) return t < 2 ? be16_byte((uint32_t)(pr & 0xffff) | 1u, t) : be16_byte((uint32_t)((pr >> 16) & 0xffff) | 1u, t - 2);
+        if (t < 12) return (int)((rnd(seed, i, 4) >> (8 * (t - 4))) & 0xff);  // seq, ack
+        switch (t) {
+            case 12: return 0x50;  // data offset 5
+            case 13: return 0x18;  // ACK | PSH
+            case 14: case 15: return be16_byte((uint32_t)((pr >> 32) & 0xffff), t - 14);
+            default: return 0;     // checksum, urgent pointer
+        }
+    }
+    return -1;
+}
+
+__device__ int ipv6_l4_byte(uint64_t seed, uint64_t i, uint32_t L, uint32_t o) {
+    const uint32_t kinds[3] = {6, 17, 58};
+    const uint32_t nh = kinds[i % 3];
+    if (o < 40) {
+        switch (o) {
+            case 0: return 0x60;
+            case 1: case 2: case 3: return 0;
+            case 4: case 5: return be16_byte(L - 40, o - 4);
+            case 6: return (int)nh;
+            case 7: return 64;
+            default: {
+                const uint32_t a = o - 8;  // 0..31: src then dst
+                return (int)((rnd(seed, i, 5 + a / 8) >> (8 * (a % 8))) & 0xff);
+            }
+        }
+    }
+    const uint32_t t = o - 40;
+    const uint64_t pr = rnd(seed, i, 3);
+    if (nh == 17) {
+        if (t >= 8) return -1;
+        switch (t) {
+            case 0: case 1: return be16_byte((uint32_t)(pr & 0xffff), t);
+            case 2: case 3: return be16_byte((uint32_t)((pr >> 16) & 0xffff) | 1u, t - 2);
+            case 4: case 5: return be16_byte(L - 40, t - 4);
+            default: return 0;
+        }
+    }
+    if (nh == 58) {
+        if (t >= 8) return -1;
+        switch (t) {
+            case 0: return 128;  // echo request
+            case 1: case 2: case 3: return 0;
+            default: return (int)((pr >> (8 * t)) & 0xff);
+        }
+    }
+    if (t >= 20) return -1;
+    if (t < 4) return t < 2 ? be16_byte((uint32_t)(pr & 0xffff) | 1u, t) : be16_byte((uint32_t)((pr >> 16) & 0xffff) | 1u, t - 2);
+    if (t < 12) return (int)((rnd(seed, i, 4) >> (8 * (t - 4))) & 0xff);
+    switch (t) {
+        case 12: return 0x50;
+        case 13: return 0x18;
+        case 14: case 15: return be16_byte((uint32_t)((pr >> 32) & 0xffff), t - 14);
+        default: return 0;
+    }
+}
+
+__device__ int header_byte(uint32_t profile, uint64_t seed, uint64_t i, uint32_t L, uint32_t o) {
+    switch (profile) {
+        case SMOL_SYNTH_UDP4: return ipv4_l4_byte(17, seed, i, L, o);
+        case SMOL_SYNTH_TCP4: return ipv4_l4_byte(6, seed, i, L, o);
+        case SMOL_SYNTH_V6MIX: return ipv6_l4_byte(seed, i, L, o);
+        case SMOL_SYNTH_ETH_TCP4:
+            if (o < 12) return (int)((rnd(seed, i, 9 + o / 6) >> (8 * (o % 6))) & 0xff) & (o == 0 || o == 6 ? 0xfe : 0xff);
+            if (o == 12) return 0x08;
+            if (o == 13) return 0x00;
+            return L >= 14 ? ipv4_l4_byte(6, seed, i, L - 14, o - 14) : -1;
+        default: return -1;
+    }
+}
+
+// One wavefront per record; lanes store consecutive bytes (64 contiguous bytes per store).
+__global__ __launch_bounds__(256) void synth_kernel(SynthParams p) {
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t i = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64; i < p.n; i += nw) {
+        uint64_t off;
+        uint32_t L;
+        if (p.desc) {
+            off = p.desc[i].offset;
+            L = p.desc[i].len;
+        } else {
+            off = i * p.stride;
+            L = p.len;
+        }
+        uint8_t* rec = p.buf + off;
+        for (uint32_t o = lane; o < L; o += 64) {
+            int b = header_byte(p.profile, p.seed, i, L, o);
+            if (b < 0) {
+                const uint64_t pos = off + o;
+                b = (int)((splitmix64(p.seed ^ (pos >> 3) * 0xD6E8FEB86659FD93ull) >> (8 * (pos & 7))) & 0xff);
+            }
+            rec[o] = (uint8_t)b;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t xorshift32(uint32_t& s) {  // fault_injector.rs:8-16
+    uint32_t x = s;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    s = x;
+    return x;
+}
+
+__global__ void corrupt_kernel(SynthParams p, uint32_t every) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j * every < p.n; j += stride) {
+        const uint64_t i = j * every;
+        uint64_t off;
+        uint32_t L;
+        if (p.desc) {
+            off = p.desc[i].offset;
+            L = p.desc[i].len;
+        } else {
+            off = i * p.stride;
+            L = p.len;
+        }
+        if (L == 0) continue;
+        uint32_t s = (uint32_t)splitmix64(p.seed ^ i) | 1u;
+        const uint32_t idx = xorshift32(s) % L;            // fault_injector.rs:48
+        const uint32_t bit = 1u << (xorshift32(s) % 8u);   // fault_injector.rs:49
+        p.buf[off + idx] ^= (uint8_t)bit;
+    }
+}
+
+hipError_t launch_synth(const SynthParams& p, uint32_t max_blocks, hipStream_t s) {
+    const uint64_t want = (p.n + 3) / 4;
+    const uint32_t blocks = (uint32_t)(want < max_blocks ? want : max_blocks);
+    hipLaunchKernelGGL(synth_kernel, dim3(blocks), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_corrupt(const SynthParams& p, uint32_t every, hipStream_t s) {
+    const uint64_t cnt = (p.n + every - 1) / every;
+    const uint64_t want = (cnt + 255) / 256;
+    const uint32_t blocks = (uint32_t)(want < 4096 ? (want ? want : 1) : 4096);
+    hipLaunchKernelGGL(corrupt_kernel, dim3(blocks), dim3(256), 0, s, p, every);
+    return hipGetLastError();
+}
+
+}  // namespace smolcsum
+
+namespace smolcsum {
+
+// Read-only HBM streaming probe: every lane reads 16-byte chunks with a grid stride and folds
+// them into a value that is stored only if it hits an impossible pattern (keeps the loads live).
+__global__ __launch_bounds__(256) void stream_read_kernel(const uint4* p, uint64_t n16, uint32_t* sink) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t acc = 0;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+        acc += (a.x ^ b.y) + (c.z ^ d.w) + (a.w ^ d.x) + (b.z ^ c.y);
+    }
+    for (; i < n16; i += stride) {
+        const uint4 a = p[i];
+        acc += a.x ^ a.y ^ a.z ^ a.w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t max_blocks,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(stream_read_kernel, dim3(max_blocks), dim3(256), 0, s,
+                       reinterpret_cast<const uint4*>(buf), bytes / 16, sink);
+    return hipGetLastError();
+}
+
+}  // namespace smolcsum

@@ -1,0 +1,194 @@
+"""Batched device checksum engine over torch device tensors (HBM-resident batches).
+
+``ChecksumEngine`` wraps one ``smol_csum_ctx_t`` (include/smolcsum.h).  Buffers are plain
+``torch.uint8`` CUDA(HIP) tensors holding packed records; ``Batch`` describes where the records
+are — a fixed stride (no descriptor traffic) or a device array of 16-byte descriptors.  Every
+call is asynchronous on the given stream (default: torch's current stream on the engine's
+device).  PyTorch is only the allocator/stream provider here; all checksum work runs in the HIP
+kernels of libsmolcsum.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import BatchC, Caps, check, lib
+from .phy import ChecksumCapabilities
+
+KIND_RAW, KIND_IP, KIND_ETH = 0, 1, 2
+
+ST_IP_OK = 0x01
+ST_L4_OK = 0x02
+ST_L4_PARTIAL = 0x04
+ST_IP_VALID = 0x08
+ST_L4_VALID = 0x10
+ST_MALFORMED = 0x20
+ST_UNSUPPORTED = 0x40
+ST_ACCEPT = 0x80
+
+SYNTH_UDP4, SYNTH_TCP4, SYNTH_V6MIX, SYNTH_ETH_TCP4, SYNTH_RANDOM = 0, 1, 2, 3, 4
+
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("kind", "u1"), ("flags", "u1"),
+                       ("reserved", "<u2")])
+assert DESC_DTYPE.itemsize == 16
+
+
+def make_descriptors(offsets, lengths, kinds) -> np.ndarray:
+    """Host array of smol_csum_desc_t (view it as uint8 and copy it to the device)."""
+    n = len(offsets)
+    d = np.zeros(n, dtype=DESC_DTYPE)
+    d["offset"] = np.asarray(offsets, dtype=np.uint64)
+    d["len"] = np.asarray(lengths, dtype=np.uint32)
+    d["kind"] = np.broadcast_to(np.asarray(kinds, dtype=np.uint8), (n,))
+    return d
+
+
+@dataclass
+class Batch:
+    """smol_csum_batch_t: ``desc`` is a device tensor of n*16 bytes, or None for a fixed stride."""
+
+    n: int
+    stride: int = 0
+    length: int = 0
+    kind: int = KIND_IP
+    desc: Optional[object] = None  # torch.Tensor (uint8, device) holding n descriptors
+
+    def c(self) -> BatchC:
+        b = BatchC()
+        b.desc = self.desc.data_ptr() if self.desc is not None else None
+        b.n = self.n
+        b.stride = self.stride
+        b.len = self.length
+        b.kind = self.kind
+        return b
+
+    @staticmethod
+    def fixed(n: int, stride: int, length: Optional[int] = None, kind: int = KIND_IP) -> "Batch":
+        return Batch(n=n, stride=stride, length=stride if length is None else length, kind=kind)
+
+    @staticmethod
+    def from_records(offsets, lengths, kinds, device) -> "Batch":
+        import torch
+
+        d = make_descriptors(offsets, lengths, kinds)
+        t = torch.from_numpy(d.view(np.uint8).copy()).to(device)
+        return Batch(n=len(d), desc=t)
+
+
+def _caps(caps) -> Caps:
+    if caps is None:
+        caps = ChecksumCapabilities()
+    tup = caps.as_tuple() if isinstance(caps, ChecksumCapabilities) else tuple(int(x) for x in caps)
+    c = Caps()
+    c.ipv4, c.udp, c.tcp, c.icmpv4, c.icmpv6 = tup
+    return c
+
+
+class ChecksumEngine:
+    """One device context.  Not thread-safe: use one engine per host thread."""
+
+    def __init__(self, device: int = 0):
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        check(lib().smol_csum_ctx_create(self.device, ctypes.byref(h)), "smol_csum_ctx_create")
+        self._h = h
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            lib().smol_csum_ctx_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- helpers ----
+    def _stream(self, stream):
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        return ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+
+    @staticmethod
+    def _check_buf(buf, batch: Batch):
+        assert buf.is_cuda and buf.dtype.itemsize == 1, "buffer must be a uint8 device tensor"
+        assert buf.is_contiguous()
+        if batch.desc is None and batch.n:
+            need = (batch.n - 1) * batch.stride + batch.length
+            assert need <= buf.numel(), f"batch needs {need} bytes, buffer has {buf.numel()}"
+
+    # ---- reference surface ----
+    def data(self, buf, batch: Batch, out=None, stream=None):
+        """out[i] = checksum::data(record i) (int16 tensor holding the u16 bit pattern)."""
+        import torch
+
+        self._check_buf(buf, batch)
+        if out is None:
+            out = torch.empty(batch.n, dtype=torch.int16, device=buf.device)
+        b = batch.c()
+        check(lib().smol_csum_batch_data(self._h, buf.data_ptr(), ctypes.byref(b), out.data_ptr(),
+                                         self._stream(stream)), "smol_csum_batch_data")
+        return out
+
+    def emit(self, buf, batch: Batch, caps=None, status=None, stream=None):
+        """In-place fill (Repr::emit gates under ``caps``); returns ``status`` (may be None)."""
+        self._check_buf(buf, batch)
+        b = batch.c()
+        c = _caps(caps)
+        check(lib().smol_csum_batch_emit(self._h, buf.data_ptr(), ctypes.byref(b), ctypes.byref(c),
+                                         status.data_ptr() if status is not None else None,
+                                         self._stream(stream)), "smol_csum_batch_emit")
+        return status
+
+    def verify(self, buf, batch: Batch, caps=None, status=None, stream=None):
+        """status[i] = SMOL_ST_* bits (Repr::parse gates under ``caps``)."""
+        import torch
+
+        self._check_buf(buf, batch)
+        if status is None:
+            status = torch.empty(batch.n, dtype=torch.uint8, device=buf.device)
+        b = batch.c()
+        c = _caps(caps)
+        check(lib().smol_csum_batch_verify(self._h, buf.data_ptr(), ctypes.byref(b), ctypes.byref(c),
+                                           status.data_ptr(), self._stream(stream)),
+              "smol_csum_batch_verify")
+        return status
+
+    # ---- tooling ----
+    def synth(self, buf, batch: Batch, profile: int, seed: int, stream=None):
+        self._check_buf(buf, batch)
+        b = batch.c()
+        check(lib().smol_csum_tool_synth(self._h, buf.data_ptr(), ctypes.byref(b), int(profile),
+                                         int(seed) & (2**64 - 1), self._stream(stream)),
+              "smol_csum_tool_synth")
+
+    def corrupt(self, buf, batch: Batch, every: int, seed: int, stream=None):
+        self._check_buf(buf, batch)
+        b = batch.c()
+        check(lib().smol_csum_tool_corrupt(self._h, buf.data_ptr(), ctypes.byref(b), int(every),
+                                           int(seed) & (2**64 - 1), self._stream(stream)),
+              "smol_csum_tool_corrupt")
+
+    def stream_read(self, buf, sink, stream=None):
+        """Read-only HBM streaming probe over the whole buffer (tooling)."""
+        nbytes = buf.numel() // 16 * 16
+        check(lib().smol_csum_tool_stream_read(self._h, buf.data_ptr(), nbytes, sink.data_ptr(),
+                                               self._stream(stream)), "smol_csum_tool_stream_read")
+
+    def set_shape(self, shape: int):
+        check(lib().smol_csum_tool_set_shape(self._h, int(shape)), "smol_csum_tool_set_shape")
+
+    def set_max_blocks(self, max_blocks: int):
+        check(lib().smol_csum_tool_set_max_blocks(self._h, int(max_blocks)),
+              "smol_csum_tool_set_max_blocks")
+
+
+def auto_shape(length: int, has_desc: bool = False) -> int:
+    return int(_lib.lib().smol_csum_tool_auto_shape(int(length), int(bool(has_desc))))

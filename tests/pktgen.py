@@ -1,0 +1,107 @@
+"""Host-side packet builders for the parity tests (plain Python/numpy, no checksum logic: every
+checksum field is written as given, usually 0)."""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle
+
+
+def be16(v: int) -> bytes:
+    return bytes([(v >> 8) & 0xFF, v & 0xFF])
+
+
+def ipv4(src: bytes, dst: bytes, proto: int, payload: bytes, ihl: int = 5, ttl: int = 64,
+         flags_frag: int = 0x4000, ident: int = 0, csum: int = 0, options: bytes | None = None,
+         total_len: int | None = None) -> bytes:
+    hl = ihl * 4
+    opts = options if options is not None else bytes(hl - 20)
+    assert len(opts) == hl - 20
+    tl = hl + len(payload) if total_len is None else total_len
+    h = bytes([0x40 | ihl, 0]) + be16(tl) + be16(ident) + be16(flags_frag) + bytes([ttl, proto]) \
+        + be16(csum) + src + dst + opts
+    return h + payload
+
+
+def ipv6(src: bytes, dst: bytes, nh: int, payload: bytes, hop: int = 64,
+         payload_len: int | None = None) -> bytes:
+    pl = len(payload) if payload_len is None else payload_len
+    return bytes([0x60, 0, 0, 0]) + be16(pl) + bytes([nh, hop]) + src + dst + payload
+
+
+def hbh(next_header: int, length_units: int, rng) -> bytes:
+    """IPv6 Hop-by-Hop header of (length_units+1)*8 bytes: PadN filler."""
+    total = (length_units + 1) * 8
+    body = bytearray(total - 2)
+    body[0] = 1  # PadN
+    body[1] = total - 4
+    return bytes([next_header, length_units]) + bytes(body)
+
+
+def udp(sport: int, dport: int, payload: bytes, csum: int = 0, length: int | None = None) -> bytes:
+    ln = 8 + len(payload) if length is None else length
+    return be16(sport) + be16(dport) + be16(ln) + be16(csum) + payload
+
+
+def tcp(sport: int, dport: int, payload: bytes, csum: int = 0, doff: int = 5, flags: int = 0x18,
+        seq: int = 1, ack: int = 2) -> bytes:
+    opts = bytes((doff - 5) * 4)
+    return be16(sport) + be16(dport) + seq.to_bytes(4, "big") + ack.to_bytes(4, "big") + \
+        bytes([doff << 4, flags]) + be16(8192) + be16(csum) + be16(0) + opts + payload
+
+
+def icmp_echo(t: int, payload: bytes, csum: int = 0) -> bytes:
+    return bytes([t, 0]) + be16(csum) + be16(0x1234) + be16(0xABCD) + payload
+
+
+def eth(payload: bytes, ethertype: int = 0x0800) -> bytes:
+    return bytes([0x02, 0, 0, 0, 0, 1, 0x02, 0, 0, 0, 0, 2]) + be16(ethertype) + payload
+
+
+def rand_bytes(rng, n: int) -> bytes:
+    return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+def pack(records, align: int = 1, gap_rng=None, base_pad: int = 0):
+    """Pack byte records into one host buffer; returns (buf, offsets, lengths).  ``gap_rng`` adds
+    random 0..7 byte gaps (odd offsets)."""
+    offs, lens, chunks, pos = [], [], [], base_pad
+    if base_pad:
+        chunks.append(bytes(base_pad))
+    for r in records:
+        gap = int(gap_rng.integers(0, 8)) if gap_rng is not None else 0
+        if gap:
+            chunks.append(bytes([0xA5]) * gap)
+            pos += gap
+        if align > 1 and pos % align:
+            pad = align - pos % align
+            chunks.append(bytes(pad))
+            pos += pad
+        offs.append(pos)
+        lens.append(len(r))
+        chunks.append(r)
+        pos += len(r)
+    chunks.append(bytes(16))  # tail slack
+    buf = np.frombuffer(b"".join(chunks), dtype=np.uint8).copy()
+    return buf, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
+
+
+def oracle_desc(offs, lens, kinds):
+    from smoltcp_amd.engine import make_descriptors
+
+    return make_descriptors(offs, lens, kinds)
+
+
+def oracle_verify_records(buf, offs, lens, kinds, caps=(0, 0, 0, 0, 0)):
+    d = oracle_desc(offs, lens, kinds)
+    return oracle.batch_verify(buf, d, len(d), caps=caps)
+
+
+def oracle_emit_records(buf, offs, lens, kinds, caps=(0, 0, 0, 0, 0)):
+    d = oracle_desc(offs, lens, kinds)
+    return oracle.batch_emit(buf, d, len(d), caps=caps)
+
+
+def oracle_data_records(buf, offs, lens):
+    d = oracle_desc(offs, lens, 0)
+    return oracle.batch_data(buf, d, len(d))
