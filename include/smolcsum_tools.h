@@ -33,9 +33,13 @@ int smol_csum_tool_synth(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_b
 int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                            uint32_t every, uint64_t seed, void* stream);
 
-/* Force a launch shape for the next batched calls on this context (-1 = automatic).
- * 0: 16 lanes x 2 chunks, 1: 32 x 3, 2: 64 x 2, 3: 64 x 4 per record step. */
+/* Force a launch shape for the next batched calls on this context (-1 = automatic).  A shape is
+ * (lanes per record) x (16-byte chunks per lane per step):
+ * 0: 8 x 6, 1: 16 x 3, 2: 16 x 6, 3: 32 x 3, 4: 32 x 4, 5: 64 x 2, 6: 64 x 4. */
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
+
+/* Non-temporal (streaming, cache-bypassing) record loads on (default) or off. */
+int smol_csum_tool_set_nontemporal(smol_csum_ctx_t* ctx, int on);
 
 /* Cap the number of workgroups per launch (0 = automatic: CUs x 8). */
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);

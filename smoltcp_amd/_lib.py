@@ -30,6 +30,7 @@ ABI_SYMBOLS = [
 ]
 TOOL_SYMBOLS = [
     "smol_csum_tool_synth", "smol_csum_tool_corrupt", "smol_csum_tool_set_shape",
+    "smol_csum_tool_set_nontemporal",
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
 ]
 
@@ -112,6 +113,8 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_tool_corrupt.restype = i32
     L.smol_csum_tool_set_shape.argtypes = [vp, i32]
     L.smol_csum_tool_set_shape.restype = i32
+    L.smol_csum_tool_set_nontemporal.argtypes = [vp, i32]
+    L.smol_csum_tool_set_nontemporal.restype = i32
     L.smol_csum_tool_set_max_blocks.argtypes = [vp, u32]
     L.smol_csum_tool_set_max_blocks.restype = i32
     L.smol_csum_tool_stream_read.argtypes = [vp, vp, u64, vp, vp]

@@ -20,6 +20,8 @@ struct smol_csum_ctx {
     int num_cu;
     uint32_t max_blocks;  // persistent-grid cap (CUs x 8 by default)
     int shape;            // -1 automatic, else CFG_*
+    bool nontemporal;     // non-temporal (streaming) loads; default on
+    uint8_t* dummy;       // 256 zero bytes on the device (target of loads with nothing to read)
 };
 
 namespace {
@@ -62,9 +64,9 @@ bool caps_valid(const smol_checksum_caps_t* c) {
 int auto_shape(uint32_t len, bool has_desc) {
     if (has_desc) return CFG_G64U4;
     const uint64_t need = (uint64_t)len + 15;  // bytes of aligned chunks a record can touch
-    if (need <= 16 * 16 * 2) return CFG_G16U2;
-    if (need <= 16 * 32 * 3) return CFG_G32U3;
-    if (need <= 16 * 64 * 2) return CFG_G64U2;
+    if (need <= 16 * 8 * 6) return CFG_G8U6;
+    if (need <= 16 * 16 * 6) return CFG_G16U6;
+    if (need <= 16 * 32 * 4) return CFG_G32U4;
     return CFG_G64U4;
 }
 
@@ -99,10 +101,11 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     }
     p.out16 = d_out;
     p.status = d_status;
+    p.dummy = ctx->dummy;
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
     const int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr);
-    hipError_t e = launch_csum(mode, shape, p, ctx->max_blocks, (hipStream_t)stream);
+    hipError_t e = launch_csum(mode, shape, ctx->nontemporal, p, ctx->max_blocks, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
     return SMOL_OK;
 }
@@ -178,17 +181,37 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     int cus = 0;
     hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
+    DeviceGuard guard(device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    uint8_t* dummy = nullptr;
+    e = hipMalloc(&dummy, 256);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+    e = hipMemset(dummy, 0, 256);
+    if (e != hipSuccess) {
+        (void)hipFree(dummy);
+        return hip_fail(e, "hipMemset");
+    }
     auto* c = new (std::nothrow) smol_csum_ctx;
-    if (!c) return SMOL_ENOMEM;
+    if (!c) {
+        (void)hipFree(dummy);
+        return SMOL_ENOMEM;
+    }
+    c->dummy = dummy;
     c->device = device;
     c->num_cu = cus;
     c->max_blocks = (uint32_t)(cus > 0 ? cus : 256) * 8u;
     c->shape = -1;
+    c->nontemporal = true;
     *out = c;
     return SMOL_OK;
 }
 
 int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
+    if (!ctx) return SMOL_OK;
+    {
+        DeviceGuard guard(ctx->device);
+        (void)hipFree(ctx->dummy);
+    }
     delete ctx;
     return SMOL_OK;
 }
@@ -254,6 +277,12 @@ int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
     if (!ctx || shape < -1 || shape >= CFG_COUNT) return SMOL_EINVAL;
     ctx->shape = shape;
+    return SMOL_OK;
+}
+
+int smol_csum_tool_set_nontemporal(smol_csum_ctx_t* ctx, int on) {
+    if (!ctx) return SMOL_EINVAL;
+    ctx->nontemporal = on != 0;
     return SMOL_OK;
 }
 

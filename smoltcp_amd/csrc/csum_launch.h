@@ -12,7 +12,16 @@ namespace smolcsum {
 enum { MODE_DATA = 0, MODE_EMIT = 1, MODE_VERIFY = 2 };
 
 // Launch shapes: lanes per record (G) x 16-byte chunks per lane per step (U).
-enum { CFG_G16U2 = 0, CFG_G32U3 = 1, CFG_G64U2 = 2, CFG_G64U4 = 3, CFG_COUNT = 4 };
+enum {
+    CFG_G8U6 = 0,
+    CFG_G16U3 = 1,
+    CFG_G16U6 = 2,
+    CFG_G32U3 = 3,
+    CFG_G32U4 = 4,
+    CFG_G64U2 = 5,
+    CFG_G64U4 = 6,
+    CFG_COUNT = 7
+};
 
 struct KParams {
     uint8_t* buf;
@@ -24,9 +33,10 @@ struct KParams {
     uint32_t caps_ipv4, caps_udp, caps_tcp, caps_icmpv4, caps_icmpv6;
     uint16_t* out16;  // MODE_DATA
     uint8_t* status;  // MODE_VERIFY (required), MODE_EMIT (optional)
+    const uint8_t* dummy;  // 16-byte-aligned device line read by loads that have nothing to read
 };
 
-hipError_t launch_csum(int mode, int cfg, const KParams& p, uint32_t max_blocks, hipStream_t s);
+hipError_t launch_csum(int mode, int shape, bool nt, const KParams& p, uint32_t max_blocks, hipStream_t s);
 
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
 struct SynthParams {

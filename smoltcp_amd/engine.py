@@ -185,6 +185,10 @@ class ChecksumEngine:
     def set_shape(self, shape: int):
         check(lib().smol_csum_tool_set_shape(self._h, int(shape)), "smol_csum_tool_set_shape")
 
+    def set_nontemporal(self, on: bool):
+        check(lib().smol_csum_tool_set_nontemporal(self._h, int(bool(on))),
+              "smol_csum_tool_set_nontemporal")
+
     def set_max_blocks(self, max_blocks: int):
         check(lib().smol_csum_tool_set_max_blocks(self._h, int(max_blocks)),
               "smol_csum_tool_set_max_blocks")

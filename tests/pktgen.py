@@ -32,9 +32,10 @@ def ipv6(src: bytes, dst: bytes, nh: int, payload: bytes, hop: int = 64,
 def hbh(next_header: int, length_units: int, rng) -> bytes:
     """IPv6 Hop-by-Hop header of (length_units+1)*8 bytes: PadN filler."""
     total = (length_units + 1) * 8
-    body = bytearray(total - 2)
-    body[0] = 1  # PadN
-    body[1] = total - 4
+    body = bytearray(total - 2)  # Pad1 options (type 0) ...
+    if total - 4 < 256:
+        body[0] = 1  # ... or one PadN option when it fits
+        body[1] = total - 4
     return bytes([next_header, length_units]) + bytes(body)
 
 

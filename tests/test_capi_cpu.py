@@ -119,11 +119,11 @@ def test_batched_calls_fail_loudly_without_a_device():
 def test_auto_shape():
     from smoltcp_amd.engine import auto_shape
 
-    assert auto_shape(64) == 0
-    assert auto_shape(1500) == 1
-    assert auto_shape(2000) == 2
-    assert auto_shape(9000) == 3
-    assert auto_shape(1500, True) == 3
+    assert auto_shape(64) == 0      # 8 lanes x 6 chunks
+    assert auto_shape(1500) == 2    # 16 lanes x 6 chunks: four 1500-byte records per wavefront
+    assert auto_shape(2000) == 4    # 32 x 4
+    assert auto_shape(9000) == 6    # 64 x 4
+    assert auto_shape(1500, True) == 6
 
 
 def test_phy_policy_mirror():

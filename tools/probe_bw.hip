@@ -1,0 +1,146 @@
+// HBM read-streaming probe for MI355X: which load form / occupancy / in-flight depth reads a
+// 1.5 GB device buffer fastest.  Standalone tool (not part of the library):
+//   hipcc -O3 --offload-arch=gfx950 tools/probe_bw.hip -o tools/probe_bw && tools/probe_bw
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                  \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess) {                                                \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                           \
+        }                                                                      \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldnt(const uint4* q) {
+    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <int UNR, bool NT>
+__global__ __launch_bounds__(256) void grid_stride(const uint4* __restrict__ p, uint64_t n16, uint32_t* sink) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t acc = 0;
+    for (; i + (UNR - 1) * stride < n16; i += UNR * stride) {
+        uint4 v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) v[u] = NT ? ldnt(p + i + u * stride) : p[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) acc += __builtin_amdgcn_sad_u16(v[u].x, 0, 0) + __builtin_amdgcn_sad_u16(v[u].y, 0, 0) + __builtin_amdgcn_sad_u16(v[u].z, 0, 0) + __builtin_amdgcn_sad_u16(v[u].w, 0, 0);
+    }
+    for (; i < n16; i += stride) acc += p[i].x;
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+// Each wave owns contiguous spans of SPAN 1-KiB pieces (like a record-per-wave kernel).
+template <int UNR, bool NT>
+__global__ __launch_bounds__(256) void wave_spans(const uint4* __restrict__ p, uint64_t n16, uint32_t* sink) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const uint64_t per = 64ull * UNR;  // 16-B chunks per wave step
+    uint32_t acc = 0;
+    for (uint64_t base = w0 * per; base + per <= n16; base += nw * per) {
+        uint4 v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) v[u] = NT ? ldnt(p + base + u * 64 + lane) : p[base + u * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) acc += __builtin_amdgcn_sad_u16(v[u].x, 0, 0) + __builtin_amdgcn_sad_u16(v[u].y, 0, 0) + __builtin_amdgcn_sad_u16(v[u].z, 0, 0) + __builtin_amdgcn_sad_u16(v[u].w, 0, 0);
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+// LDS-DMA: each wave streams 1 KiB pieces into its own LDS ring with global_load_lds_dwordx4,
+// DEPTH pieces in flight, then sums them with ds_read_b128.
+template <int DEPTH>
+__global__ __launch_bounds__(256) void glds_ring(const uint4* __restrict__ p, uint64_t n16, uint32_t* sink) {
+    __shared__ uint4 ring[4][DEPTH][64];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x / 64;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = (uint64_t)blockIdx.x * 4 + w;
+    const uint64_t npieces = n16 / 64;
+    uint32_t acc = 0;
+    uint64_t issue = w0, consume = w0;
+    int slot_i = 0, slot_c = 0;
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+        if (issue < npieces) {
+            __builtin_amdgcn_global_load_lds((const void*)(p + issue * 64 + lane), (__attribute__((address_space(3))) void*)&ring[w][slot_i][0], 16, 0, 0);
+        }
+        issue += nw;
+        slot_i = (slot_i + 1) % DEPTH;
+    }
+    while (consume < npieces) {
+        __builtin_amdgcn_s_waitcnt(0x0F70 | ((DEPTH - 1) & 0xF) | (((DEPTH - 1) >> 4) << 14));  // vmcnt(DEPTH-1)
+        __builtin_amdgcn_wave_barrier();
+        uint4 v = ring[w][slot_c][lane];
+        acc += __builtin_amdgcn_sad_u16(v.x, 0, 0) + __builtin_amdgcn_sad_u16(v.y, 0, 0) + __builtin_amdgcn_sad_u16(v.z, 0, 0) + __builtin_amdgcn_sad_u16(v.w, 0, 0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): slot read before it is refilled
+        __builtin_amdgcn_wave_barrier();
+        if (issue < npieces) {
+            __builtin_amdgcn_global_load_lds((const void*)(p + issue * 64 + lane), (__attribute__((address_space(3))) void*)&ring[w][slot_c][0], 16, 0, 0);
+        }
+        issue += nw;
+        consume += nw;
+        slot_c = (slot_c + 1) % DEPTH;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+template <class K>
+static double time_kernel(K k, int blocks, const uint4* p, uint64_t n16, uint32_t* sink, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, p, n16, sink);
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, p, n16, sink);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    CK(hipGetLastError());
+    return ms / reps;
+}
+
+int main(int argc, char** argv) {
+    const uint64_t bytes = argc > 1 ? strtoull(argv[1], 0, 0) : 1572864000ull;
+    const uint64_t n16 = bytes / 16;
+    uint4* p;
+    uint32_t* sink;
+    CK(hipMalloc(&p, n16 * 16));
+    CK(hipMalloc(&sink, 4));
+    CK(hipMemset(p, 0x5a, n16 * 16));
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    printf("bytes=%llu CUs=%d\n", (unsigned long long)(n16 * 16), cus);
+    const int reps = 20;
+    auto rep = [&](const char* name, int bpc, double ms) {
+        printf("%-28s blocks/CU=%-3d %8.4f ms  %7.1f GB/s\n", name, bpc, ms, n16 * 16 / ms / 1e6);
+    };
+    for (int bpc : {2, 4, 8, 16}) {
+        const int blocks = cus * bpc;
+        rep("grid_stride U1", bpc, time_kernel(grid_stride<1, false>, blocks, p, n16, sink, reps));
+        rep("grid_stride U4", bpc, time_kernel(grid_stride<4, false>, blocks, p, n16, sink, reps));
+        rep("grid_stride U8", bpc, time_kernel(grid_stride<8, false>, blocks, p, n16, sink, reps));
+        rep("grid_stride U4 nt", bpc, time_kernel(grid_stride<4, true>, blocks, p, n16, sink, reps));
+        rep("grid_stride U8 nt", bpc, time_kernel(grid_stride<8, true>, blocks, p, n16, sink, reps));
+        rep("wave_spans U2", bpc, time_kernel(wave_spans<2, false>, blocks, p, n16, sink, reps));
+        rep("wave_spans U4", bpc, time_kernel(wave_spans<4, false>, blocks, p, n16, sink, reps));
+        rep("wave_spans U8", bpc, time_kernel(wave_spans<8, false>, blocks, p, n16, sink, reps));
+        rep("wave_spans U4 nt", bpc, time_kernel(wave_spans<4, true>, blocks, p, n16, sink, reps));
+        rep("wave_spans U8 nt", bpc, time_kernel(wave_spans<8, true>, blocks, p, n16, sink, reps));
+        rep("glds_ring D4", bpc, time_kernel(glds_ring<4>, blocks, p, n16, sink, reps));
+        rep("glds_ring D8", bpc, time_kernel(glds_ring<8>, blocks, p, n16, sink, reps));
+    }
+    CK(hipFree(p));
+    return 0;
+}
