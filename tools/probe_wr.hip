@@ -1,0 +1,79 @@
+// Write-pattern probe: a 1536-B-record stream (16 lanes x 6 nt dwordx4 per record) with one of
+// several per-record store patterns, to price in-place checksum-field writes.  Standalone tool.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+#define GMEM __attribute__((address_space(1)))
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void scatter(uint8_t* buf, uint64_t n, const uint32_t* vals) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = vals[r];
+        *(GMEM uint16_t*)((uint64_t)buf + r * 1536 + 10) = (uint16_t)v;
+        *(GMEM uint16_t*)((uint64_t)buf + r * 1536 + 26) = (uint16_t)(v >> 16);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void rw(uint8_t* buf, uint64_t n, uint8_t* status) {
+    const int lane = threadIdx.x & 15;
+    const uint64_t ng = (uint64_t)gridDim.x * 16;
+    for (uint64_t r = (uint64_t)blockIdx.x * 16 + threadIdx.x / 16; r < n; r += ng) {
+        const uint64_t a0 = (uint64_t)buf + r * 1536;
+        u32x4 v[6];
+#pragma unroll
+        for (int u = 0; u < 6; ++u) v[u] = __builtin_nontemporal_load((const GMEM u32x4*)(a0 + 16 * (u * 16 + lane)));
+        uint32_t acc = 0;
+#pragma unroll
+        for (int u = 0; u < 6; ++u) acc = __builtin_amdgcn_sad_u16(v[u].x, 0, __builtin_amdgcn_sad_u16(v[u].y, 0, __builtin_amdgcn_sad_u16(v[u].z, 0, __builtin_amdgcn_sad_u16(v[u].w, 0, acc))));
+        acc += __shfl_xor(acc, 1, 16); acc += __shfl_xor(acc, 2, 16); acc += __shfl_xor(acc, 4, 16); acc += __shfl_xor(acc, 8, 16);
+        if (MODE == 1 && lane == 0) { *(GMEM uint16_t*)(a0 + 10) = (uint16_t)acc; *(GMEM uint16_t*)(a0 + 26) = (uint16_t)(acc >> 16); }
+        if (MODE == 2 && lane < 2) { u32x4 c = v[0]; c.x = acc; *(GMEM u32x4*)(a0 + 16 * lane) = c; }          // 32 B
+        if (MODE == 3 && lane < 4) { u32x4 c = v[0]; c.x = acc; *(GMEM u32x4*)(a0 + 16 * lane) = c; }                                   // 64 B line
+        if (MODE == 4 && lane < 8) { u32x4 c = v[0]; c.x = acc; *(GMEM u32x4*)(a0 + 16 * lane) = c; }                                   // 128 B
+        if (MODE == 5 && lane == 0) { status[r] = (uint8_t)acc; }
+        if (MODE == 6 && lane == 0) { u32x4 c = v[0]; c.x = acc; *(GMEM u32x4*)(a0) = c; }                                             // 16 B
+        if (MODE == 7 && lane == 0) { __builtin_nontemporal_store((uint16_t)acc, (GMEM uint16_t*)(a0 + 10)); __builtin_nontemporal_store((uint16_t)(acc >> 16), (GMEM uint16_t*)(a0 + 26)); }
+        if (MODE == 8 && lane == 0) { *(GMEM uint32_t*)((uint64_t)status + 4 * r) = acc; }   // compact 4-B array
+        if (MODE == 0 && acc == 0x12345678u) status[0] = 1;
+    }
+}
+
+int main() {
+    const uint64_t n = 1 << 20;
+    uint8_t *buf, *st;
+    CK(hipMalloc(&buf, n * 1536));
+    CK(hipMalloc(&st, 4 * n));
+    CK(hipMemset(buf, 0x33, n * 1536));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    const char* names[] = {"read only", "2 x 2-B stores", "32-B store", "64-B line store", "128-B store", "1-B status array", "16-B store", "2 x 2-B nt stores", "4-B compact array", "scatter kernel only"};
+    for (int rnd = 0; rnd < 2; ++rnd)
+    for (int bpc : {2, 8}) for (int m = 0; m < 10; ++m) {
+        auto run = [&]() {
+            switch (m) {
+                case 0: hipLaunchKernelGGL(rw<0>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 1: hipLaunchKernelGGL(rw<1>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 2: hipLaunchKernelGGL(rw<2>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 3: hipLaunchKernelGGL(rw<3>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 4: hipLaunchKernelGGL(rw<4>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 5: hipLaunchKernelGGL(rw<5>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 6: hipLaunchKernelGGL(rw<6>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 7: hipLaunchKernelGGL(rw<7>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 8: hipLaunchKernelGGL(rw<8>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                default: hipLaunchKernelGGL(scatter, dim3(256 * bpc), dim3(256), 0, 0, buf, n, (const uint32_t*)st); break;
+            }
+        };
+        for (int i = 0; i < 3; ++i) run();
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < 10; ++i) run();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b)); ms /= 10;
+        if (rnd) printf("%-20s blocks/CU=%d %8.4f ms %7.1f GB/s(read)\n", names[m], bpc, ms, n * 1536 / ms / 1e6);
+    }
+    CK(hipGetLastError());
+    return 0;
+}
