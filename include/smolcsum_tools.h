@@ -38,8 +38,13 @@ int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum
  * 0: 8 x 6, 1: 16 x 3, 2: 16 x 6, 3: 32 x 3, 4: 32 x 4, 5: 64 x 2, 6: 64 x 4. */
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
-/* Non-temporal (streaming, cache-bypassing) record loads on (default) or off. */
-int smol_csum_tool_set_nontemporal(smol_csum_ctx_t* ctx, int on);
+/* Kernel variant (-1 = automatic per mode, the default): 0 = non-temporal loads + register
+ * prefetch of the next step,
+ * 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch. */
+int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
+
+/* Emit as read pass + scatter pass, or (default) with the field stores inside the read pass. */
+int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int on);
 
 /* Cap the number of workgroups per launch (0 = automatic: CUs x 8). */
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);

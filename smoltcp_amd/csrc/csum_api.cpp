@@ -20,8 +20,11 @@ struct smol_csum_ctx {
     int num_cu;
     uint32_t max_blocks;  // persistent-grid cap (CUs x 8 by default)
     int shape;            // -1 automatic, else CFG_*
-    bool nontemporal;     // non-temporal (streaming) loads; default on
+    int variant;          // kernel variant: 0 nt + prefetch (default), 1 plain + prefetch, 2 nt only
     uint8_t* dummy;       // 256 zero bytes on the device (target of loads with nothing to read)
+    bool defer_emit;      // emit = read pass into a patch array + scatter pass (default off)
+    uint64_t* patch;      // emit workspace: one u64 per record of a chunk
+    uint64_t patch_cap;   // records the workspace holds
 };
 
 namespace {
@@ -82,6 +85,24 @@ int check_batch(const smol_csum_batch_t* b, const void* d_buf) {
     return SMOL_OK;
 }
 
+// Emit workspace: records per deferred-emit chunk (8 B each: 64 MiB at the cap).
+constexpr uint64_t SMOL_EMIT_CHUNK = 1ull << 23;
+
+int reserve_patch(smol_csum_ctx_t* ctx, uint64_t n) {
+    if (n <= ctx->patch_cap) return SMOL_OK;
+    DeviceGuard guard(ctx->device);
+    if (ctx->patch) (void)hipFree(ctx->patch);
+    ctx->patch = nullptr;
+    ctx->patch_cap = 0;
+    hipError_t e = hipMalloc(&ctx->patch, n * sizeof(uint64_t));
+    if (e != hipSuccess) {
+        ctx->patch = nullptr;
+        return hip_fail(e, "hipMalloc (emit workspace)");
+    }
+    ctx->patch_cap = n;
+    return SMOL_OK;
+}
+
 int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t* b,
         const smol_checksum_caps_t* caps, uint16_t* d_out, uint8_t* d_status, void* stream) {
     KParams p;
@@ -104,9 +125,37 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.dummy = ctx->dummy;
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
-    const int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr);
-    hipError_t e = launch_csum(mode, shape, ctx->nontemporal, p, ctx->max_blocks, (hipStream_t)stream);
-    if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
+    int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr);
+    // Measured on MI355X (tools/sweep.py, C2): emit runs fastest with cached loads and 8-lane
+    // groups (its in-place field writes dominate), verify / data with non-temporal loads.
+    int variant = ctx->variant;
+    if (variant < 0) {
+        variant = mode == MODE_EMIT ? 1 : 0;
+        if (mode == MODE_EMIT && ctx->shape < 0 && shape == CFG_G16U6) shape = CFG_G8U6;
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    if (mode != MODE_EMIT || !ctx->defer_emit) {
+        hipError_t e = launch_csum(mode, shape, variant, p, ctx->max_blocks, s);
+        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
+        return SMOL_OK;
+    }
+    // Deferred emit: read pass -> patch array, then the scatter pass, in chunks of at most
+    // SMOL_EMIT_CHUNK records (the workspace is reserved once per context).
+    const uint64_t cap = b->n < SMOL_EMIT_CHUNK ? b->n : SMOL_EMIT_CHUNK;
+    int rc = reserve_patch(ctx, cap);
+    if (rc != SMOL_OK) return rc;
+    for (uint64_t start = 0; start < b->n; start += cap) {
+        KParams q = p;
+        q.n = (b->n - start) < cap ? (b->n - start) : cap;
+        if (b->desc) q.desc = b->desc + start;
+        else q.buf = d_buf + start * b->stride;
+        if (d_status) q.status = d_status + start;
+        q.patch = ctx->patch;
+        hipError_t e = launch_csum(MODE_EMIT, shape, variant, q, ctx->max_blocks, s);
+        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
+        e = launch_scatter(q, ctx->max_blocks, s);
+        if (e != hipSuccess) return hip_fail(e, "scatter kernel launch");
+    }
     return SMOL_OK;
 }
 
@@ -197,13 +246,21 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
         return SMOL_ENOMEM;
     }
     c->dummy = dummy;
+    c->defer_emit = false;
+    c->patch = nullptr;
+    c->patch_cap = 0;
     c->device = device;
     c->num_cu = cus;
     c->max_blocks = (uint32_t)(cus > 0 ? cus : 256) * 8u;
     c->shape = -1;
-    c->nontemporal = true;
+    c->variant = -1;
     *out = c;
     return SMOL_OK;
+}
+
+int smol_csum_ctx_reserve(smol_csum_ctx_t* ctx, uint64_t max_records) {
+    if (!ctx) return SMOL_EINVAL;
+    return reserve_patch(ctx, max_records < SMOL_EMIT_CHUNK ? max_records : SMOL_EMIT_CHUNK);
 }
 
 int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
@@ -211,6 +268,7 @@ int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
     {
         DeviceGuard guard(ctx->device);
         (void)hipFree(ctx->dummy);
+        if (ctx->patch) (void)hipFree(ctx->patch);
     }
     delete ctx;
     return SMOL_OK;
@@ -280,9 +338,15 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
     return SMOL_OK;
 }
 
-int smol_csum_tool_set_nontemporal(smol_csum_ctx_t* ctx, int on) {
+int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
+    if (!ctx || variant < -1 || variant > 2) return SMOL_EINVAL;
+    ctx->variant = variant;
+    return SMOL_OK;
+}
+
+int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int on) {
     if (!ctx) return SMOL_EINVAL;
-    ctx->nontemporal = on != 0;
+    ctx->defer_emit = on != 0;
     return SMOL_OK;
 }
 

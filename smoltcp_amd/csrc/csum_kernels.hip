@@ -140,6 +140,13 @@ __device__ __forceinline__ uint32_t sum_masked_words(const u32x4& c, int lo, int
     return add_words(mask_dword(c.w, lo - 12, hi - 12), acc);
 }
 
+// Emit patch word, one per record when the field writes are deferred to scatter_kernel:
+// bits 0-15 IPv4 header checksum, 16-31 L4 checksum, 32-55 L4 field offset in the record,
+// PATCH_IP / PATCH_L4 = write that field, PATCH_ETH = the IPv4 header sits behind Ethernet.
+constexpr uint64_t PATCH_IP = 1ull << 56;
+constexpr uint64_t PATCH_L4 = 1ull << 57;
+constexpr uint64_t PATCH_ETH = 1ull << 58;
+
 // Per-group walk state.
 struct Walk {
     uint64_t r;      // current record
@@ -153,7 +160,7 @@ struct Walk {
 
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
-template <int G, int U, int MODE, bool IMPLICIT, bool NT>
+template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)[U], u32x4 (&nx)[U],
                                           int lane, uint64_t ngroups, u32x4* win) {
     const uint8_t* winb = reinterpret_cast<const uint8_t*>(win);
@@ -164,7 +171,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
     const RecRef rec2 = last ? w.nxt : w.cur;
     const uint32_t nch2 = last ? n_chunks(w.nxt) : w.nch;
     const uint32_t step2 = last ? 0u : w.step + 1;
-    load_step<G, U, NT>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
+    if (PF) load_step<G, U, NT>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
@@ -263,13 +270,16 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
             psum = group_sum<G>(psum);
             if (lane == 0) {
                 const gu8 wrec = (gu8)w.cur.a0;
+                (void)wrec;
                 uint32_t st = g.st;
                 // IPv4 header: data(header) (canonical fold of the big-endian word sum)
                 uint32_t ip_valid = 1, ip_ok = 1;
+                uint64_t patch = 0;  // emit: the field writes of this record (see PATCH_* below)
                 if (g.fam == 4) {
                     const uint32_t hdr = fold32(hsum);
                     if (MODE == MODE_EMIT) {
-                        store_be16(wrec + g.ip_off + 10, caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u);
+                        const uint32_t v = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
+                        patch |= (uint64_t)v | PATCH_IP | (g.ip_off ? PATCH_ETH : 0ull);
                     } else {
                         ip_valid = hdr == 0xffffu;
                         ip_ok = caps_rx(p.caps_ipv4) ? ip_valid : 1u;
@@ -308,7 +318,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
                         const bool fill = g.proto == P_IGMP ? true : caps_tx(gate_caps);
                         uint32_t c = ~comb & 0xffffu;
                         if (g.proto == P_UDP && c == 0) c = 0xffffu;  // udp.rs:207
-                        store_be16(wrec + fpos, fill ? c : 0u);
+                        patch |= ((uint64_t)(fill ? c : 0u) << 16) | ((uint64_t)fpos << 32) | PATCH_L4;
                     } else {
                         l4_valid = comb == 0xffffu;
                         if (g.proto == P_UDP && field == 0) l4_valid = 1;  // udp.rs:138-140
@@ -317,6 +327,13 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
                     }
                 }
                 if (MODE == MODE_EMIT) {
+                    if (p.patch) {
+                        // deferred: the scatter pass writes the fields after every read is done
+                        ((GMEM uint64_t*)p.patch)[r] = patch;
+                    } else {
+                        if (patch & PATCH_IP) store_be16(wrec + g.ip_off + 10, (uint32_t)(patch & 0xffffu));
+                        if (patch & PATCH_L4) store_be16(wrec + ((patch >> 32) & 0xffffffu), (uint32_t)((patch >> 16) & 0xffffu));
+                    }
                     if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
                 } else {
                     const bool mal = (st & SMOL_ST_MALFORMED) != 0;
@@ -341,8 +358,12 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
 }
 
 // MODE_DATA: checksum::data over [0, len).  MODE_EMIT / MODE_VERIFY: the protocol gates.
-template <int G, int U, int MODE, bool IMPLICIT, bool NT>
+// VAR: 0 = non-temporal loads + register prefetch (default), 1 = plain loads + prefetch,
+// 2 = non-temporal loads, no prefetch (each step loads then waits; occupancy hides latency).
+template <int G, int U, int MODE, bool IMPLICIT, int VAR>
 __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
+    constexpr bool NT = VAR != 1;
+    constexpr bool PF = VAR != 2;
     constexpr int GPB = 256 / G;
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     __shared__ u32x4 win[GPB][WIN_BYTES / 16];
@@ -361,57 +382,100 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     w.s1 = 0;
     w.acc = w.acc2 = 0;
 
-    u32x4 va[U], vb[U];
-    load_step<G, U, NT>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
-    // the body is instantiated twice with the register sets' roles swapped
-    while (true) {
-        if (!walk_step<G, U, MODE, IMPLICIT, NT>(p, w, va, vb, lane, ngroups, &win[gib][0])) break;
-        if (!walk_step<G, U, MODE, IMPLICIT, NT>(p, w, vb, va, lane, ngroups, &win[gib][0])) break;
+    u32x4 va[U];
+    if (PF) {
+        u32x4 vb[U];
+        load_step<G, U, NT>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
+        // the body is instantiated twice with the register sets' roles swapped
+        while (true) {
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, vb, lane, ngroups, &win[gib][0])) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, vb, va, lane, ngroups, &win[gib][0])) break;
+        }
+    } else {
+        while (true) {
+            load_step<G, U, NT>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy);
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, va, lane, ngroups, &win[gib][0])) break;
+        }
     }
+}
+
+// Second pass of a deferred emit: one lane per record applies the patch word.  Writing the 2-byte
+// fields inside the read pass interleaves a scattered write with every 1.5 KB of streamed reads,
+// which cost ~40 % of a read pass on MI355X (tools/probe_wr.hip); a compact patch array (+5 %)
+// plus this write-only pass is far cheaper.
+template <bool IMPLICIT>
+__global__ __launch_bounds__(256) void scatter_kernel(KParams p) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += stride) {
+        const uint64_t patch = ((const GMEM uint64_t*)p.patch)[r];
+        if (!(patch & (PATCH_IP | PATCH_L4))) continue;
+        uint64_t a0;
+        if (IMPLICIT) {
+            a0 = (uint64_t)p.buf + r * p.stride;
+        } else {
+            const GMEM uint64_t* d = (const GMEM uint64_t*)((uint64_t)p.desc + 16 * r);
+            a0 = (uint64_t)p.buf + d[0];
+        }
+        if (patch & PATCH_IP) store_be16((gu8)(a0 + ((patch & PATCH_ETH) ? 24 : 10)), (uint32_t)(patch & 0xffffu));
+        if (patch & PATCH_L4) store_be16((gu8)(a0 + ((patch >> 32) & 0xffffffu)), (uint32_t)((patch >> 16) & 0xffffu));
+    }
+}
+
+hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    const uint64_t want = (p.n + 255) / 256;
+    const uint32_t blocks = (uint32_t)(want < max_blocks ? want : max_blocks);
+    if (p.desc) hipLaunchKernelGGL(scatter_kernel<false>, dim3(blocks), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(scatter_kernel<true>, dim3(blocks), dim3(256), 0, s, p);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
 // Launch table
 // ---------------------------------------------------------------------------------------------
 
-template <int G, int U, int MODE, bool IMPLICIT, bool NT>
+template <int G, int U, int MODE, bool IMPLICIT, int VAR>
 static hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = (uint32_t)(want < max_blocks ? want : max_blocks);
-    hipLaunchKernelGGL((csum_kernel<G, U, MODE, IMPLICIT, NT>), dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((csum_kernel<G, U, MODE, IMPLICIT, VAR>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
-template <int MODE, bool IMPLICIT, bool NT>
+template <int MODE, bool IMPLICIT, int VAR>
 static hipError_t launch_shape(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (shape) {
-        case CFG_G8U6: return launch_one<8, 6, MODE, IMPLICIT, NT>(p, max_blocks, s);
-        case CFG_G16U3: return launch_one<16, 3, MODE, IMPLICIT, NT>(p, max_blocks, s);
-        case CFG_G16U6: return launch_one<16, 6, MODE, IMPLICIT, NT>(p, max_blocks, s);
-        case CFG_G32U3: return launch_one<32, 3, MODE, IMPLICIT, NT>(p, max_blocks, s);
-        case CFG_G32U4: return launch_one<32, 4, MODE, IMPLICIT, NT>(p, max_blocks, s);
-        case CFG_G64U2: return launch_one<64, 2, MODE, IMPLICIT, NT>(p, max_blocks, s);
-        default: return launch_one<64, 4, MODE, IMPLICIT, NT>(p, max_blocks, s);
+        case CFG_G8U6: return launch_one<8, 6, MODE, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G16U3: return launch_one<16, 3, MODE, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G16U6: return launch_one<16, 6, MODE, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G32U3: return launch_one<32, 3, MODE, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G32U4: return launch_one<32, 4, MODE, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G64U2: return launch_one<64, 2, MODE, IMPLICIT, VAR>(p, max_blocks, s);
+        default: return launch_one<64, 4, MODE, IMPLICIT, VAR>(p, max_blocks, s);
     }
 }
 
 template <int MODE>
-static hipError_t launch_mode(int shape, bool nt, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+static hipError_t launch_mode(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const bool implicit = p.desc == nullptr;
-    if (nt) {
-        return implicit ? launch_shape<MODE, true, true>(shape, p, max_blocks, s)
-                        : launch_shape<MODE, false, true>(shape, p, max_blocks, s);
+    switch (var) {
+        case 1:
+            return implicit ? launch_shape<MODE, true, 1>(shape, p, max_blocks, s)
+                            : launch_shape<MODE, false, 1>(shape, p, max_blocks, s);
+        case 2:
+            return implicit ? launch_shape<MODE, true, 2>(shape, p, max_blocks, s)
+                            : launch_shape<MODE, false, 2>(shape, p, max_blocks, s);
+        default:
+            return implicit ? launch_shape<MODE, true, 0>(shape, p, max_blocks, s)
+                            : launch_shape<MODE, false, 0>(shape, p, max_blocks, s);
     }
-    return implicit ? launch_shape<MODE, true, false>(shape, p, max_blocks, s)
-                    : launch_shape<MODE, false, false>(shape, p, max_blocks, s);
 }
 
-hipError_t launch_csum(int mode, int shape, bool nt, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (mode) {
-        case MODE_DATA: return launch_mode<MODE_DATA>(shape, nt, p, max_blocks, s);
-        case MODE_EMIT: return launch_mode<MODE_EMIT>(shape, nt, p, max_blocks, s);
-        default: return launch_mode<MODE_VERIFY>(shape, nt, p, max_blocks, s);
+        case MODE_DATA: return launch_mode<MODE_DATA>(shape, var, p, max_blocks, s);
+        case MODE_EMIT: return launch_mode<MODE_EMIT>(shape, var, p, max_blocks, s);
+        default: return launch_mode<MODE_VERIFY>(shape, var, p, max_blocks, s);
     }
 }
 

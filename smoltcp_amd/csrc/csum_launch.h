@@ -34,9 +34,11 @@ struct KParams {
     uint16_t* out16;  // MODE_DATA
     uint8_t* status;  // MODE_VERIFY (required), MODE_EMIT (optional)
     const uint8_t* dummy;  // 16-byte-aligned device line read by loads that have nothing to read
+    uint64_t* patch;       // MODE_EMIT: deferred field writes (one u64 per record) or nullptr
 };
 
-hipError_t launch_csum(int mode, int shape, bool nt, const KParams& p, uint32_t max_blocks, hipStream_t s);
+hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s);
+hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s);
 
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
 struct SynthParams {

@@ -185,9 +185,15 @@ class ChecksumEngine:
     def set_shape(self, shape: int):
         check(lib().smol_csum_tool_set_shape(self._h, int(shape)), "smol_csum_tool_set_shape")
 
-    def set_nontemporal(self, on: bool):
-        check(lib().smol_csum_tool_set_nontemporal(self._h, int(bool(on))),
-              "smol_csum_tool_set_nontemporal")
+    def set_variant(self, variant: int):
+        check(lib().smol_csum_tool_set_variant(self._h, int(variant)), "smol_csum_tool_set_variant")
+
+    def set_deferred_emit(self, on: bool):
+        check(lib().smol_csum_tool_set_deferred_emit(self._h, int(bool(on))),
+              "smol_csum_tool_set_deferred_emit")
+
+    def reserve(self, max_records: int):
+        check(lib().smol_csum_ctx_reserve(self._h, int(max_records)), "smol_csum_ctx_reserve")
 
     def set_max_blocks(self, max_blocks: int):
         check(lib().smol_csum_tool_set_max_blocks(self._h, int(max_blocks)),

@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--shapes", default="0,1,2,3,4,5,6")
     ap.add_argument("--blocks", default="0")
-    ap.add_argument("--nt", default="1,0")
+    ap.add_argument("--var", default="0,1,2")
+    ap.add_argument("--defer", default="1")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     eng = E.ChecksumEngine(0)
@@ -36,10 +37,13 @@ def main():
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     for rnd in range(2):
         for shape in [int(x) for x in args.shapes.split(",")]:
-            for nt in [int(x) for x in args.nt.split(",")]:
-                for bpc in [int(x) for x in args.blocks.split(",")]:
+            for var, bpc, defer in [(a, b, c) for a in [int(x) for x in args.var.split(",")]
+                                   for b in [int(x) for x in args.blocks.split(",")]
+                                   for c in [int(x) for x in args.defer.split(",")]]:
+                if True:
+                    eng.set_deferred_emit(bool(defer))
                     eng.set_shape(shape)
-                    eng.set_nontemporal(bool(nt))
+                    eng.set_variant(var)
                     eng.set_max_blocks(bpc * cus)
                     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                     for _ in range(2):
@@ -55,14 +59,14 @@ def main():
                     torch.cuda.synchronize()
                     em = ev[0].elapsed_time(ev[1]) / args.reps
                     vm = ev[1].elapsed_time(ev[2]) / args.reps
-                    row = {"round": rnd, "shape": shape, "nt": nt, "blocks_per_cu": bpc,
+                    row = {"round": rnd, "shape": shape, "var": var, "blocks_per_cu": bpc, "defer": defer,
                            "emit_ms": round(em, 4), "verify_ms": round(vm, 4),
                            "emit_GBs": round(wl.read_bytes / em / 1e6, 1),
                            "verify_GBs": round(wl.read_bytes / vm / 1e6, 1)}
                     rows.append(row)
                     print(json.dumps(row), flush=True)
     eng.set_shape(-1)
-    eng.set_nontemporal(True)
+    eng.set_variant(-1)
     eng.set_max_blocks(0)
 
 
