@@ -164,10 +164,10 @@ typedef struct smol_csum_ctx smol_csum_ctx_t;
 int smol_csum_ctx_create(int device, smol_csum_ctx_t** out);
 int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx);
 
-/* Reserve the emit workspace for batches of up to `max_records` records (8 bytes per record,
- * capped at 2^23 records; larger batches are processed in chunks).  Optional: the first
- * smol_csum_batch_emit on a context reserves it on demand, which allocates device memory and so
- * must not happen inside a HIP graph capture — call this first when capturing. */
+/* Reserve the deferred-emit workspace for batches of up to `max_records` records (8 bytes per
+ * record, capped at 2^23 records; larger batches are processed in chunks).  Only needed with the
+ * deferred emit (smolcsum_tools.h): its first call would otherwise allocate device memory, which
+ * must not happen inside a HIP graph capture. */
 int smol_csum_ctx_reserve(smol_csum_ctx_t* ctx, uint64_t max_records);
 
 /* checksum::data() over every record span; d_out[i] = data(record i) (u16, numeric value as the
@@ -178,8 +178,8 @@ int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
 /* In-place emit: for every record write the IPv4 header checksum and the L4 checksum the way the
  * reference's Repr::emit does under `caps` (fill when tx(), else 0; UDP 0 -> 0xffff; IGMP always
  * filled).  `d_status` (nullable) receives SMOL_ST_MALFORMED / SMOL_ST_UNSUPPORTED per record.
- * Implemented as a read pass that records the field values in the context's workspace followed
- * by a write pass (two kernels on `stream`); records must not overlap. */
+ * One kernel on `stream` (or, when selected with smol_csum_tool_set_deferred_emit, a read pass
+ * into the context's workspace plus a write pass); records must not overlap. */
 int smol_csum_batch_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                          const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
 

@@ -40,8 +40,14 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
 /* Kernel variant (-1 = automatic per mode, the default): 0 = non-temporal loads + register
  * prefetch of the next step,
- * 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch. */
+ * 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch (the "walk"
+ * kernel: a group parses and finishes its own record); 3 / 4 = the "tile" kernel (groups only
+ * stream and sum, lanes finish 64 records at once) with non-temporal / plain loads — emit and
+ * verify only (data() always uses the walk kernel). */
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
+
+/* Tile kernel: records per wavefront tile, 32 (default) or 64. */
+int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records);
 
 /* Emit as read pass + scatter pass, or (default) with the field stores inside the read pass. */
 int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int on);

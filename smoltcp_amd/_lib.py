@@ -30,7 +30,7 @@ ABI_SYMBOLS = [
 ]
 TOOL_SYMBOLS = [
     "smol_csum_tool_synth", "smol_csum_tool_corrupt", "smol_csum_tool_set_shape",
-    "smol_csum_tool_set_variant", "smol_csum_tool_set_deferred_emit",
+    "smol_csum_tool_set_variant", "smol_csum_tool_set_deferred_emit", "smol_csum_tool_set_tile",
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
 ]
 
@@ -119,6 +119,8 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_tool_set_shape.restype = i32
     L.smol_csum_tool_set_variant.argtypes = [vp, i32]
     L.smol_csum_tool_set_variant.restype = i32
+    L.smol_csum_tool_set_tile.argtypes = [vp, i32]
+    L.smol_csum_tool_set_tile.restype = i32
     L.smol_csum_tool_set_max_blocks.argtypes = [vp, u32]
     L.smol_csum_tool_set_max_blocks.restype = i32
     L.smol_csum_tool_stream_read.argtypes = [vp, vp, u64, vp, vp]

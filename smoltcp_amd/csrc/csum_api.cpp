@@ -18,14 +18,29 @@ using namespace smolcsum;
 struct smol_csum_ctx {
     int device;
     int num_cu;
-    uint32_t max_blocks;  // persistent-grid cap (CUs x 8 by default)
+    uint32_t max_blocks;  // grid cap (kNaturalGrid: one work item per group)
     int shape;            // -1 automatic, else CFG_*
     int variant;          // kernel variant: 0 nt + prefetch (default), 1 plain + prefetch, 2 nt only
     uint8_t* dummy;       // 256 zero bytes on the device (target of loads with nothing to read)
     bool defer_emit;      // emit = read pass into a patch array + scatter pass (default off)
     uint64_t* patch;      // emit workspace: one u64 per record of a chunk
     uint64_t patch_cap;   // records the workspace holds
+    int tile_records;     // tile kernel: records per wavefront tile (32 or 64)
+    bool max_blocks_set;  // grid cap given explicitly (tooling)
 };
+
+namespace smolcsum {
+
+uint32_t resident_blocks(const void* kernel, uint32_t num_cu, uint32_t max_blocks) {
+    if (num_cu == 0) return max_blocks;  // explicit grid cap (smol_csum_tool_set_max_blocks)
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const uint64_t cap = (uint64_t)per_cu * num_cu;
+    return (uint32_t)(cap < max_blocks ? cap : max_blocks);
+}
+
+}  // namespace smolcsum
 
 namespace {
 
@@ -64,10 +79,15 @@ bool caps_valid(const smol_checksum_caps_t* c) {
     return c->reserved[0] == 0 && c->reserved[1] == 0 && c->reserved[2] == 0;
 }
 
+// Grid cap meaning "one work item per group" (no persistent loop): on MI355X many small
+// workgroups dispatched by the hardware beat a persistent grid (tools/sweep.py, C2: verify
+// 0.244 ms vs 0.27 ms at 8 blocks per CU).
+constexpr uint32_t kNaturalGrid = 0x7fffffffu;
+
 int auto_shape(uint32_t len, bool has_desc) {
-    if (has_desc) return CFG_G64U4;
+    if (has_desc) return CFG_G16U3;
     const uint64_t need = (uint64_t)len + 15;  // bytes of aligned chunks a record can touch
-    if (need <= 16 * 8 * 6) return CFG_G8U6;
+    if (need <= 16 * 8 * 6 * 2) return CFG_G8U6;
     if (need <= 16 * 16 * 6) return CFG_G16U6;
     if (need <= 16 * 32 * 4) return CFG_G32U4;
     return CFG_G64U4;
@@ -123,17 +143,25 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.out16 = d_out;
     p.status = d_status;
     p.dummy = ctx->dummy;
+    p.num_cu = ctx->max_blocks_set ? 0u : (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
     int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr);
     // Measured on MI355X (tools/sweep.py, C2): emit runs fastest with cached loads and 8-lane
     // groups (its in-place field writes dominate), verify / data with non-temporal loads.
+    // Variants: 0-2 = walk kernel (csum_kernels.hip: nt + prefetch / plain + prefetch / nt),
+    // 3-4 = tile kernel (csum_tile.hip: nt / plain loads), emit and verify only.
     int variant = ctx->variant;
-    if (variant < 0) {
-        variant = mode == MODE_EMIT ? 1 : 0;
-        if (mode == MODE_EMIT && ctx->shape < 0 && shape == CFG_G16U6) shape = CFG_G8U6;
-    }
+    if (variant < 0) variant = 1;  // walk kernel, cached loads + prefetch (measured best, C2-C4)
+    if (mode == MODE_DATA && variant > 2) variant = 0;
+    const bool use_tile = variant >= 3;
     const hipStream_t s = (hipStream_t)stream;
+    if (use_tile && !(mode == MODE_EMIT && ctx->defer_emit)) {
+        hipError_t e = launch_tile(mode, shape, variant - 3, ctx->tile_records, p, ctx->max_blocks, s);
+        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
+        return SMOL_OK;
+    }
+    if (use_tile) variant = 0;
     if (mode != MODE_EMIT || !ctx->defer_emit) {
         hipError_t e = launch_csum(mode, shape, variant, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
@@ -247,11 +275,13 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     }
     c->dummy = dummy;
     c->defer_emit = false;
+    c->tile_records = 32;
+    c->max_blocks_set = false;
     c->patch = nullptr;
     c->patch_cap = 0;
     c->device = device;
     c->num_cu = cus;
-    c->max_blocks = (uint32_t)(cus > 0 ? cus : 256) * 8u;
+    c->max_blocks = kNaturalGrid;
     c->shape = -1;
     c->variant = -1;
     *out = c;
@@ -339,8 +369,14 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 2) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 4) return SMOL_EINVAL;
     ctx->variant = variant;
+    return SMOL_OK;
+}
+
+int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records) {
+    if (!ctx || (records != 32 && records != 64)) return SMOL_EINVAL;
+    ctx->tile_records = records;
     return SMOL_OK;
 }
 
@@ -352,7 +388,8 @@ int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int on) {
 
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks) {
     if (!ctx) return SMOL_EINVAL;
-    ctx->max_blocks = max_blocks ? max_blocks : (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * 8u;
+    ctx->max_blocks = max_blocks ? max_blocks : kNaturalGrid;
+    ctx->max_blocks_set = max_blocks != 0;
     return SMOL_OK;
 }
 
@@ -361,7 +398,8 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
     if (!ctx || !d_buf || !d_sink || (bytes & 15u) || ((uintptr_t)d_buf & 15u)) return SMOL_EINVAL;
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
-    hipError_t e = launch_stream_read(d_buf, bytes, d_sink, ctx->max_blocks, (hipStream_t)stream);
+    hipError_t e = launch_stream_read(d_buf, bytes, d_sink, (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * 8u,
+                                      (hipStream_t)stream);
     return e == hipSuccess ? SMOL_OK : hip_fail(e, "stream-read kernel launch");
 }
 

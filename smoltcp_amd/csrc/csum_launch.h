@@ -35,10 +35,17 @@ struct KParams {
     uint8_t* status;  // MODE_VERIFY (required), MODE_EMIT (optional)
     const uint8_t* dummy;  // 16-byte-aligned device line read by loads that have nothing to read
     uint64_t* patch;       // MODE_EMIT: deferred field writes (one u64 per record) or nullptr
+    uint32_t num_cu;       // compute units of the device (grid sizing)
 };
+
+// Workgroups of `kernel` (256 threads) resident on the whole device, capped at max_blocks.
+uint32_t resident_blocks(const void* kernel, uint32_t num_cu, uint32_t max_blocks);
 
 hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s);
 hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s);
+// Tile kernel (csum_tile.hip), emit / verify only; var 0 = non-temporal loads, 1 = plain loads.
+hipError_t launch_tile(int mode, int shape, int var, int tile_records, const KParams& p, uint32_t max_blocks,
+                       hipStream_t s);
 
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
 struct SynthParams {

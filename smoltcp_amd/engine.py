@@ -195,6 +195,9 @@ class ChecksumEngine:
     def reserve(self, max_records: int):
         check(lib().smol_csum_ctx_reserve(self._h, int(max_records)), "smol_csum_ctx_reserve")
 
+    def set_tile(self, records: int):
+        check(lib().smol_csum_tool_set_tile(self._h, int(records)), "smol_csum_tool_set_tile")
+
     def set_max_blocks(self, max_blocks: int):
         check(lib().smol_csum_tool_set_max_blocks(self._h, int(max_blocks)),
               "smol_csum_tool_set_max_blocks")
