@@ -28,6 +28,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from smoltcp_amd import shard as S  # noqa: E402
+
 METRIC = "GiB/s checksummed (device-resident), batched 1500B segments, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 GIB = float(1 << 30)
@@ -59,7 +61,7 @@ class Workload:
 
         self.cfg = cfg
         self.E = E
-        seed = {"c2": 0x5EED0001, "c3": 0x5EED0002, "c4": 0x5EED0003, "c5": 0x5EED0005}[cfg] + 1000 * rank
+        seed = S.rank_seed({"c2": 0x5EED0001, "c3": 0x5EED0002, "c4": 0x5EED0003, "c5": 0x5EED0005}[cfg], rank)
         self.seed = seed
         if cfg in ("c2", "c5"):
             self.n = n or (1 << 20 if cfg == "c2" else 128 << 20)
@@ -169,9 +171,7 @@ def main():
 
     from smoltcp_amd import engine as E
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = S.dist_env()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -211,11 +211,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = S.max_over_ranks(time.perf_counter() - t0, device=dev)
 
     emit_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     verify_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
@@ -245,8 +241,7 @@ def main():
         cpu = cpu_baseline(E, wl, args.cpu_seconds)
 
     if rank == 0:
-        per_step_bytes = 2 * wl.span_bytes * world
-        value = per_step_bytes * args.steps / elapsed / GIB
+        value = S.aggregate_rate(2 * wl.span_bytes, world, args.steps, elapsed)
         # roofline of the dominant kernel: algorithmic bytes per launch / its mean launch time
         kernels = {
             "emit": {"ms": emit_ms, "bytes": wl.read_bytes + wl.desc_bytes + 4 * wl.n},

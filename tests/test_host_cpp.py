@@ -1,0 +1,73 @@
+"""The C++ host-side mirror (smoltcp_amd/host/smoltcp_checksum.hpp) through tests/cpp/test_host_mirror.
+
+CPU: the scalar mirrors against oracle-computed values (data / combine / pseudo_header incl. the
+family-mismatch error), the phy policy mirror, and Engine() failing with SMOL_ENODEV (no CPU
+fallback).  GPU: an offloading device's TX (emit) and RX (verify) over host frames, checked with the
+scalar gates on the host.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import pyref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CPP = os.path.join(ROOT, "tests", "cpp")
+BIN = os.path.join(CPP, "test_host_mirror")
+
+
+@pytest.fixture(scope="module")
+def binary():
+    subprocess.run(["make", "-s", "-C", CPP], check=True)
+    return BIN
+
+
+def _has_gpu():
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def test_cpp_scalar_mirrors(binary, tmp_path, golden):
+    rng = np.random.default_rng(5)
+    lines = []
+    spans = [b"", b"\x00", b"\xff", bytes(131074), b"\xff" * 131075]
+    spans += [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(0, 3000, 200)]
+    spans += [bytes.fromhex(k["bytes"]) for k in golden["kat"]]
+    for s in spans:
+        lines.append(f"data {s.hex() or '-'} {pyref.data(s)}")
+    for _ in range(100):
+        ws = [int(x) for x in rng.integers(0, 65536, int(rng.integers(0, 9)))]
+        lines.append(f"comb {pyref.combine(ws)} " + " ".join(map(str, ws)))
+    for _ in range(100):
+        for n in (4, 16):
+            a = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            nh, ln = int(rng.integers(256)), int(rng.integers(0, 1 << 32))
+            lines.append(f"ph {a.hex()} {b.hex()} {nh} {ln} {pyref.pseudo_header(a, b, nh, ln)}")
+    lines.append(f"ph {bytes(4).hex()} {bytes(16).hex()} 6 0 65536")  # mismatch -> error
+    p = tmp_path / "vectors.txt"
+    p.write_text("\n".join(lines) + "\n")
+    r = subprocess.run([binary, "vectors", str(p)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"vectors {len(lines)}" in r.stdout
+
+
+def test_cpp_engine_fails_loudly_without_device(binary):
+    if _has_gpu():
+        pytest.skip("a GPU is present")
+    r = subprocess.run([binary, "nodev"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_offload_device_roundtrip(binary):
+    assert _has_gpu()
+    r = subprocess.run([binary, "offload", "20011"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "emitted all valid" in r.stdout
