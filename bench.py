@@ -42,7 +42,8 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--n", type=int, default=0, help="records per GPU (default: the config's)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (0: skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
     ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
     ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
     return ap.parse_args()
@@ -111,43 +112,83 @@ class Workload:
         self.est = None
 
 
+def _oracle_pass(oracle, tx, rx, desc, m, stride, L, kind, caps, threads, pool):
+    """One emit(tx) + verify(rx) pass of the oracle over m records, split over `threads` host
+    threads (ctypes releases the GIL inside the C calls).  Returns the verify status array."""
+    bounds = [S.shard_range(m, t, threads) for t in range(threads)]
+
+    def run(lo_hi):
+        lo, hi = lo_hi
+        if hi == lo:
+            return np.zeros(0, np.uint8)
+        if desc is None:
+            a, b = lo * stride, (hi - 1) * stride + L
+            oracle.batch_emit(tx[a:b], None, hi - lo, stride, L, kind, caps)
+            return oracle.batch_verify(rx[a:b], None, hi - lo, stride, L, kind, caps)
+        oracle.batch_emit(tx, desc[lo:hi], hi - lo, 0, 0, kind, caps)
+        return oracle.batch_verify(rx, desc[lo:hi], hi - lo, 0, 0, kind, caps)
+
+    if threads == 1:
+        return run(bounds[0])
+    return np.concatenate(list(pool.map(run, bounds)))
+
+
 def cpu_baseline(E, wl, seconds: float):
-    """The oracle (a C restatement of smoltcp's scalar checksum + gates, 1 thread) over a bounded
-    sample of the same workload, timed on this host."""
+    """cpu_baseline leg: the oracle (a C restatement of smoltcp's scalar checksum + gates) timed on
+    this host over a bounded sample of the same workload, on 1 thread and on all the host threads
+    this process may use.  The oracle is also the checker here: its emit of the sample (emit is
+    idempotent) must reproduce the device's emitted bytes and its verify the device's status
+    bytes, bit for bit."""
+    import concurrent.futures as cf
+
+    import torch
+
     import oracle
 
     if seconds <= 0:
-        return None
+        return None, None
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
     if wl.batch.desc is None:
         L = wl.batch.length
-        m = min(wl.n, 32768)
-        tx = wl.tx[: m * L].cpu().numpy().copy()
-        rx = wl.rx[: m * L].cpu().numpy().copy()
-        desc = None
-        stride = L
+        m = min(wl.n, 8192 * threads)
+        end = (m - 1) * L + L
+        desc, stride = None, L
         span = wl.span_bytes * m // wl.n
     else:
-        m = min(wl.n, 8192)
+        m = min(wl.n, 2048 * threads)
         d = wl.batch.desc[: 16 * m].cpu().numpy().view(E.DESC_DTYPE).copy()
         end = int(d["offset"][-1] + d["len"][-1])
-        tx = wl.tx[:end].cpu().numpy().copy()
-        rx = wl.rx[:end].cpu().numpy().copy()
         desc, stride, L = d, 0, 0
         span = int(d["len"].astype(np.uint64).sum())
+    dev_tx = wl.tx[:end].cpu().numpy()
+    dev_st = wl.status[:m].cpu().numpy()
+    tx = dev_tx.copy()
+    rx = wl.rx[:end].cpu().numpy().copy()
     caps = (0, 0, 0, 0, 0)
     oracle.lib()
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        oracle.batch_emit(tx, desc, m, stride, L, wl.kind, caps)
-        oracle.batch_verify(rx, desc, m, stride, L, wl.kind, caps)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    gibs = 2 * span * reps / el / GIB
-    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{m} records of the same workload (emit tx + verify rx), {reps} passes in {el:.1f} s, "
-                      f"oracle/csum_oracle.c (gcc -O3 -march=x86-64-v3), 1 thread"}
+    res = {}
+    st = None
+    with cf.ThreadPoolExecutor(threads) as pool:
+        for t in sorted({1, threads}):
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                st = _oracle_pass(oracle, tx, rx, desc, m, stride, L, wl.kind, caps, t, pool)
+                reps += 1
+                el = time.perf_counter() - t0
+                if el >= seconds / 2:
+                    break
+            res[t] = (2 * span * reps / el / GIB, reps, el)
+    torch.cuda.synchronize()
+    parity = {"records": m, "emit_bitexact": bool(np.array_equal(tx, dev_tx)),
+              "verify_bitexact": bool(np.array_equal(st, dev_st)),
+              "checker": "oracle/csum_oracle.c on the cpu_baseline sample"}
+    v, reps, el = res[threads]
+    out = {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "single_core_value": round(res[1][0], 3),
+           "sample": f"{m} records of the same workload (emit tx + verify rx), {reps} passes in {el:.1f} s on "
+                     f"{threads} threads; oracle/csum_oracle.c (gcc -O3 -march=x86-64-v3), records split "
+                     f"evenly over the threads"}
+    return out, parity
 
 
 def load_traffic(cfg: str, kernel: str):
@@ -236,9 +277,9 @@ def main():
         probe = {"kernel": "stream_read_kernel", "bytes": wl.rx.numel() // 16 * 16, "ms": round(ms, 4),
                  "GB/s": round(wl.rx.numel() / ms / 1e6, 1)}
 
-    cpu = None
+    cpu, parity = None, None
     if rank == 0 and world == 1:
-        cpu = cpu_baseline(E, wl, args.cpu_seconds)
+        cpu, parity = cpu_baseline(E, wl, args.cpu_seconds)
 
     if rank == 0:
         value = S.aggregate_rate(2 * wl.span_bytes, world, args.steps, elapsed)
@@ -273,6 +314,7 @@ def main():
             "kernels_ms": {k: round(v["ms"], 4) for k, v in kernels.items()},
             "verify_rejected": rejected,
             "cpu_baseline": cpu,
+            "parity_sample": parity,
         }
         if probe:
             out["stream_read_probe"] = probe

@@ -71,3 +71,19 @@ def test_cpp_offload_device_roundtrip(binary):
     r = subprocess.run([binary, "offload", "20011"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "emitted all valid" in r.stdout
+
+
+@pytest.mark.gpu
+def test_loopback_ring_c1_analogue():
+    """tools/loopback_ring (OffloadRing: pinned ring -> HBM -> emit / verify -> host): every
+    emitted frame passes both the GPU verify and the host scalar gates."""
+    import json
+
+    assert _has_gpu()
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools"), "loopback_ring"], check=True)
+    r = subprocess.run([os.path.join(ROOT, "tools", "loopback_ring"), "70001", "1"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["gpu_offload"]["accepted"] == 70001
+    assert out["cpu_inline_1thread"]["accepted"] == 70001

@@ -22,6 +22,8 @@ for c in c2 c3 c4; do
 done
 step e2e 400 python tools/e2e.py
 tail -1 $O/e2e.log
+step loopback 400 tools/loopback_ring 262144 5
+tail -1 $O/loopback.log
 for c in ${PROF_CONFIGS:-c2 c3 c4}; do
     step kt_$c 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof/$c/kt -o run -- python3 bench.py --config $c --steps 20 --cpu-seconds 0
     step fetch_$c 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof/$c/fetch -o run -- python3 bench.py --config $c --steps 5 --warmup 1 --cpu-seconds 0
