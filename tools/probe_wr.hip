@@ -37,6 +37,13 @@ __global__ __launch_bounds__(256) void rw(uint8_t* buf, uint64_t n, uint8_t* sta
         if (MODE == 6 && lane == 0) { u32x4 c = v[0]; c.x = acc; *(GMEM u32x4*)(a0) = c; }                                             // 16 B
         if (MODE == 7 && lane == 0) { __builtin_nontemporal_store((uint16_t)acc, (GMEM uint16_t*)(a0 + 10)); __builtin_nontemporal_store((uint16_t)(acc >> 16), (GMEM uint16_t*)(a0 + 26)); }
         if (MODE == 8 && lane == 0) { *(GMEM uint32_t*)((uint64_t)status + 4 * r) = acc; }   // compact 4-B array
+        // cache-policy variants of the 2 x 2-B stores (gfx950 sc0/sc1/nt bits)
+        if (MODE == 9 && lane == 0) { asm volatile("global_store_short %0, %1, off sc0 sc1\n\tglobal_store_short %0, %2, off offset:16 sc0 sc1" :: "v"(a0 + 10), "v"(acc), "v"(acc >> 16) : "memory"); }
+        if (MODE == 10 && lane == 0) { asm volatile("global_store_short %0, %1, off sc1\n\tglobal_store_short %0, %2, off offset:16 sc1" :: "v"(a0 + 10), "v"(acc), "v"(acc >> 16) : "memory"); }
+        if (MODE == 11 && lane == 0) { asm volatile("global_store_short %0, %1, off nt sc0 sc1\n\tglobal_store_short %0, %2, off offset:16 nt sc0 sc1" :: "v"(a0 + 10), "v"(acc), "v"(acc >> 16) : "memory"); }
+        if (MODE == 12 && lane == 0) { asm volatile("global_store_short %0, %1, off sc0\n\tglobal_store_short %0, %2, off offset:16 sc0" :: "v"(a0 + 10), "v"(acc), "v"(acc >> 16) : "memory"); }
+        // one 32-B aligned sector (two 16-B stores), write-through
+        if (MODE == 13 && lane < 2) { u32x4 c = v[0]; c.x = acc; asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(a0 + 16 * lane), "v"(c) : "memory"); }
         if (MODE == 0 && acc == 0x12345678u) status[0] = 1;
     }
 }
@@ -49,9 +56,10 @@ int main() {
     CK(hipMemset(buf, 0x33, n * 1536));
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-    const char* names[] = {"read only", "2 x 2-B stores", "32-B store", "64-B line store", "128-B store", "1-B status array", "16-B store", "2 x 2-B nt stores", "4-B compact array", "scatter kernel only"};
+    const char* names[] = {"read only", "2 x 2-B stores", "32-B store", "64-B line store", "128-B store", "1-B status array", "16-B store", "2 x 2-B nt stores", "4-B compact array", "scatter kernel only",
+                           "2x2-B sc0 sc1", "2x2-B sc1", "2x2-B nt sc0 sc1", "2x2-B sc0", "32-B sc0 sc1"};
     for (int rnd = 0; rnd < 2; ++rnd)
-    for (int bpc : {2, 8}) for (int m = 0; m < 10; ++m) {
+    for (int bpc : {2, 8}) for (int m = 0; m < 15; ++m) {
         auto run = [&]() {
             switch (m) {
                 case 0: hipLaunchKernelGGL(rw<0>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
@@ -63,6 +71,11 @@ int main() {
                 case 6: hipLaunchKernelGGL(rw<6>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 case 7: hipLaunchKernelGGL(rw<7>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 case 8: hipLaunchKernelGGL(rw<8>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 10: hipLaunchKernelGGL(rw<9>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 11: hipLaunchKernelGGL(rw<10>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 12: hipLaunchKernelGGL(rw<11>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 13: hipLaunchKernelGGL(rw<12>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 14: hipLaunchKernelGGL(rw<13>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 default: hipLaunchKernelGGL(scatter, dim3(256 * bpc), dim3(256), 0, 0, buf, n, (const uint32_t*)st); break;
             }
         };
