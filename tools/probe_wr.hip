@@ -44,6 +44,11 @@ __global__ __launch_bounds__(256) void rw(uint8_t* buf, uint64_t n, uint8_t* sta
         if (MODE == 12 && lane == 0) { asm volatile("global_store_short %0, %1, off sc0\n\tglobal_store_short %0, %2, off offset:16 sc0" :: "v"(a0 + 10), "v"(acc), "v"(acc >> 16) : "memory"); }
         // one 32-B aligned sector (two 16-B stores), write-through
         if (MODE == 13 && lane < 2) { u32x4 c = v[0]; c.x = acc; asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(a0 + 16 * lane), "v"(c) : "memory"); }
+        // write density: the 2 x 2-B stores on every 2nd / 4th record only
+        if (MODE == 14 && lane == 0 && (r & 1) == 0) { *(GMEM uint16_t*)(a0 + 10) = (uint16_t)acc; *(GMEM uint16_t*)(a0 + 26) = (uint16_t)(acc >> 16); }
+        if (MODE == 15 && lane == 0 && (r & 3) == 0) { *(GMEM uint16_t*)(a0 + 10) = (uint16_t)acc; *(GMEM uint16_t*)(a0 + 26) = (uint16_t)(acc >> 16); }
+        // 64-B line store at every 2nd record
+        if (MODE == 16 && lane < 4 && (r & 1) == 0) { u32x4 c = v[0]; c.x = acc; *(GMEM u32x4*)(a0 + 16 * lane) = c; }
         if (MODE == 0 && acc == 0x12345678u) status[0] = 1;
     }
 }
@@ -57,9 +62,10 @@ int main() {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     const char* names[] = {"read only", "2 x 2-B stores", "32-B store", "64-B line store", "128-B store", "1-B status array", "16-B store", "2 x 2-B nt stores", "4-B compact array", "scatter kernel only",
-                           "2x2-B sc0 sc1", "2x2-B sc1", "2x2-B nt sc0 sc1", "2x2-B sc0", "32-B sc0 sc1"};
+                           "2x2-B sc0 sc1", "2x2-B sc1", "2x2-B nt sc0 sc1", "2x2-B sc0", "32-B sc0 sc1",
+                           "2x2-B every 2nd", "2x2-B every 4th", "64-B every 2nd"};
     for (int rnd = 0; rnd < 2; ++rnd)
-    for (int bpc : {2, 8}) for (int m = 0; m < 15; ++m) {
+    for (int bpc : {2, 8}) for (int m = 0; m < 18; ++m) {
         auto run = [&]() {
             switch (m) {
                 case 0: hipLaunchKernelGGL(rw<0>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
@@ -76,6 +82,9 @@ int main() {
                 case 12: hipLaunchKernelGGL(rw<11>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 case 13: hipLaunchKernelGGL(rw<12>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 case 14: hipLaunchKernelGGL(rw<13>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 15: hipLaunchKernelGGL(rw<14>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 16: hipLaunchKernelGGL(rw<15>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 17: hipLaunchKernelGGL(rw<16>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 default: hipLaunchKernelGGL(scatter, dim3(256 * bpc), dim3(256), 0, 0, buf, n, (const uint32_t*)st); break;
             }
         };
