@@ -16,6 +16,15 @@ __global__ void scatter(uint8_t* buf, uint64_t n, const uint32_t* vals) {
     }
 }
 
+// write-through variant of the scatter pass (sc0 sc1: the stores go to memory, not parked in L2)
+__global__ void scatter_wt(uint8_t* buf, uint64_t n, const uint32_t* vals) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = vals[r];
+        asm volatile("global_store_short %0, %1, off sc0 sc1\n\tglobal_store_short %0, %2, off offset:16 sc0 sc1"
+                     :: "v"((uint64_t)buf + r * 1536 + 10), "v"(v), "v"(v >> 16) : "memory");
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void rw(uint8_t* buf, uint64_t n, uint8_t* status) {
     const int lane = threadIdx.x & 15;
@@ -95,6 +104,39 @@ int main() {
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b)); ms /= 10;
         if (rnd) printf("%-20s blocks/CU=%d %8.4f ms %7.1f GB/s(read)\n", names[m], bpc, ms, n * 1536 / ms / 1e6);
+    }
+    // Sequences like the bench step (emit on A, then verify = read-only pass on B), so that write-backs
+    // leaking into the next kernel are counted.
+    uint8_t* bufB;
+    CK(hipMalloc(&bufB, n * 1536));
+    CK(hipMemset(bufB, 0x44, n * 1536));
+    const char* seqn[] = {"B read only", "A read + B read", "A 2x2B + B read", "A 64B + B read", "A compact + scatter + B read",
+                          "A compact + scatter_wt + B read", "A 2x2B sc0sc1 + B read", "A compact + scatter", "A compact + scatter_wt"};
+    for (int rnd = 0; rnd < 2; ++rnd)
+    for (int q = 0; q < 9; ++q) {
+        const int bpc = 2;
+        auto run = [&]() {
+            dim3 g(256 * bpc), b(256);
+            switch (q) {
+                case 0: break;
+                case 1: hipLaunchKernelGGL(rw<0>, g, b, 0, 0, buf, n, st); break;
+                case 2: hipLaunchKernelGGL(rw<1>, g, b, 0, 0, buf, n, st); break;
+                case 3: hipLaunchKernelGGL(rw<3>, g, b, 0, 0, buf, n, st); break;
+                case 4: case 7: hipLaunchKernelGGL(rw<8>, g, b, 0, 0, buf, n, st);
+                        hipLaunchKernelGGL(scatter, g, b, 0, 0, buf, n, (const uint32_t*)st); break;
+                case 5: case 8: hipLaunchKernelGGL(rw<8>, g, b, 0, 0, buf, n, st);
+                        hipLaunchKernelGGL(scatter_wt, g, b, 0, 0, buf, n, (const uint32_t*)st); break;
+                case 6: hipLaunchKernelGGL(rw<9>, g, b, 0, 0, buf, n, st); break;
+            }
+            if (q < 7) hipLaunchKernelGGL(rw<0>, g, b, 0, 0, bufB, n, st);
+        };
+        for (int i = 0; i < 3; ++i) run();
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < 10; ++i) run();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b)); ms /= 10;
+        if (rnd) printf("SEQ %-34s %8.4f ms\n", seqn[q], ms);
     }
     CK(hipGetLastError());
     return 0;
