@@ -40,7 +40,7 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "c2copy"])
     ap.add_argument("--n", type=int, default=0, help="records per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
@@ -62,10 +62,12 @@ class Workload:
 
         self.cfg = cfg
         self.E = E
-        seed = S.rank_seed({"c2": 0x5EED0001, "c3": 0x5EED0002, "c4": 0x5EED0003, "c5": 0x5EED0005}[cfg], rank)
+        seed = S.rank_seed({"c2": 0x5EED0001, "c3": 0x5EED0002, "c4": 0x5EED0003, "c5": 0x5EED0005,
+                            "c2copy": 0x5EED0006}[cfg], rank)
         self.seed = seed
-        if cfg in ("c2", "c5"):
-            self.n = n or (1 << 20 if cfg == "c2" else 128 << 20)
+        self.copy = None
+        if cfg in ("c2", "c5", "c2copy"):
+            self.n = n or (128 << 20 if cfg == "c5" else 1 << 20)
             L = 1500
             self.kind, self.profile = E.KIND_IP, E.SYNTH_UDP4
             self.batch = E.Batch.fixed(self.n, L, L, E.KIND_IP)
@@ -75,7 +77,9 @@ class Workload:
             self.desc_bytes = 0
             self.workload = (f"C2: {self.n} x 1500 B IPv4/UDP datagrams, fixed stride, emit (tx) + "
                              f"verify (rx, 1/64 single-bit corrupted)") if cfg == "c2" else \
-                (f"C5: {self.n} x 1500 B IPv4/UDP per GPU, in-place emit + verify of one batch")
+                (f"C5: {self.n} x 1500 B IPv4/UDP per GPU, in-place emit + verify of one batch") if cfg == "c5" else \
+                (f"C2copy: C2 with the TX payloads (1472 B each) copied from a separate socket buffer by the "
+                 f"fused copy + emit (UdpRepr::emit), + verify (rx)")
         elif cfg == "c3":
             self.n = n or (1 << 20)
             rng = np.random.default_rng(seed)
@@ -101,6 +105,13 @@ class Workload:
             self.workload = f"C4: {self.n} IPv6 packets (40 B header + 1280 B TCP/UDP/ICMPv6 round-robin)"
         self.tx = torch.empty(self.total, dtype=torch.uint8, device=dev)
         eng.synth(self.tx, self.batch, self.profile, seed)
+        if cfg == "c2copy":
+            # payloads live in a socket-buffer-like source, back to back; headers are in the records
+            self.src = torch.randint(0, 256, (self.n * 1472 + 16,), dtype=torch.uint8, device=dev)
+            cp = E.make_copies(np.arange(self.n, dtype=np.uint64) * 1472, 28, 1472)
+            self.copy = torch.from_numpy(cp.view(np.uint8).copy()).to(dev)
+            self.read_bytes = self.n * (28 + 1472)   # headers from the record, payload from the source
+            self.write_bytes_tx = self.n * (1472 + 4)
         if cfg == "c5":
             self.rx = self.tx
         else:
@@ -230,7 +241,10 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        eng.emit(wl.tx, wl.batch, stream=stream)
+        if wl.copy is not None:
+            eng.copy_emit(wl.tx, wl.batch, wl.src, wl.copy, stream=stream)
+        else:
+            eng.emit(wl.tx, wl.batch, stream=stream)
         if ev is not None:
             ev[1].record(stream)
         eng.verify(wl.rx, wl.batch, status=wl.status, stream=stream)
@@ -277,8 +291,28 @@ def main():
         probe = {"kernel": "stream_read_kernel", "bytes": wl.rx.numel() // 16 * 16, "ms": round(ms, 4),
                  "GB/s": round(wl.rx.numel() / ms / 1e6, 1)}
 
+    unfused = None
+    if wl.copy is not None and rank == 0:
+        # the unfused TX path for comparison: payload copy (strided device copy) then emit
+        dst = wl.tx.view(wl.n, 1500)[:, 28:]
+        srcv = wl.src[: wl.n * 1472].view(wl.n, 1472)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(2):
+            dst.copy_(srcv)
+            eng.emit(wl.tx, wl.batch, stream=stream)
+        a.record(stream)
+        for _ in range(args.steps):
+            dst.copy_(srcv)
+            eng.emit(wl.tx, wl.batch, stream=stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        unfused = {"tx_ms": round(a.elapsed_time(b) / args.steps, 4),
+                   "what": "payload copy (torch strided copy_) + smol_csum_batch_emit, same batch"}
+        eng.copy_emit(wl.tx, wl.batch, wl.src, wl.copy, stream=stream)  # leave the fused result in place
+        torch.cuda.synchronize()
+
     cpu, parity = None, None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and wl.copy is None:
         cpu, parity = cpu_baseline(E, wl, args.cpu_seconds)
 
     if rank == 0:
@@ -288,6 +322,9 @@ def main():
             "emit": {"ms": emit_ms, "bytes": wl.read_bytes + wl.desc_bytes + 4 * wl.n},
             "verify": {"ms": verify_ms, "bytes": wl.read_bytes + wl.desc_bytes + wl.n},
         }
+        if wl.copy is not None:  # fused copy + emit: headers + payload read once, payload written once
+            kernels["emit"]["bytes"] = wl.read_bytes + wl.write_bytes_tx
+            kernels["verify"]["bytes"] = wl.n * 1500 + wl.n
         dom = max(kernels, key=lambda k: kernels[k]["ms"])
         kd = kernels[dom]
         achieved = kd["bytes"] / (kd["ms"] * 1e-3) / 1e9
@@ -318,6 +355,8 @@ def main():
         }
         if probe:
             out["stream_read_probe"] = probe
+        if unfused:
+            out["unfused_tx"] = unfused
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

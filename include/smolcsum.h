@@ -188,6 +188,27 @@ int smol_csum_batch_verify(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
                            const smol_csum_batch_t* batch, const smol_checksum_caps_t* caps,
                            uint8_t* d_status, void* stream);
 
+/* Payload copy of one record for smol_csum_batch_copy_emit (16 bytes, device memory). */
+typedef struct {
+    uint64_t src_offset; /* payload position in the source buffer (any alignment)          */
+    uint32_t dst_offset; /* where the payload goes inside the record                         */
+    uint32_t len;        /* payload bytes (0: nothing to copy)                               */
+} smol_csum_copy_t;
+
+/* Fused payload copy + emit: the TcpRepr::emit / UdpRepr::emit sequence "copy the payload into
+ * the packet, then fill the checksum" (src/wire/tcp.rs:1087-1095, src/wire/udp.rs:300-308) in one
+ * pass.  For every record i: copy d_src[copy[i].src_offset ..][.. len] to record bytes
+ * [dst_offset, dst_offset + len), then emit exactly as smol_csum_batch_emit does (the headers in
+ * front of the payload were already written by the caller).  The payload is read once and
+ * written once; nothing is read back.  The result is bit-identical to a memcpy followed by
+ * smol_csum_batch_emit, including when the copied range covers a checksum field (the emitted
+ * field wins).  A record whose copy range does not fit (dst_offset + len > record length) is
+ * left untouched and reported SMOL_ST_MALFORMED.  `d_copy` is a 16-byte-aligned device array of
+ * n entries; the source must not overlap the batch buffer. */
+int smol_csum_batch_copy_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
+                              const uint8_t* d_src, const smol_csum_copy_t* d_copy,
+                              const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
+
 /* Message of the last SMOL_EHIP error on this thread ("" if none). */
 const char* smol_csum_last_error(void);
 

@@ -101,6 +101,9 @@ def lib() -> ctypes.CDLL:
     L.oracle_batch_verify.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                       ctypes.c_uint8, ctypes.POINTER(CapsC), u8p]
     L.oracle_batch_verify.restype = None
+    L.oracle_batch_copy_emit.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                         ctypes.c_uint8, ctypes.POINTER(CapsC), u8p, u8p, u8p]
+    L.oracle_batch_copy_emit.restype = None
     _LIB = L
     return L
 
@@ -137,6 +140,21 @@ def batch_emit(buf: np.ndarray, desc, n: int, stride: int = 0, length: int = 0, 
     c = caps_c(caps)
     lib().oracle_batch_emit(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride, length,
                             kind, ctypes.byref(c), _ptr(st))
+    return st
+
+
+COPY_DTYPE = np.dtype([("src_offset", "<u8"), ("dst_offset", "<u4"), ("len", "<u4")])
+
+
+def batch_copy_emit(buf: np.ndarray, desc, n: int, src: np.ndarray, copy: np.ndarray, stride: int = 0,
+                    length: int = 0, kind: int = 1, caps=(0, 0, 0, 0, 0)):
+    """memcpy of each record's payload from ``src`` (``copy``: COPY_DTYPE array), then the record
+    emit; in place on ``buf``.  Returns the status array."""
+    st = np.zeros(n, dtype=np.uint8)
+    c = caps_c(caps)
+    copy = np.ascontiguousarray(copy, dtype=COPY_DTYPE)
+    lib().oracle_batch_copy_emit(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride, length,
+                                 kind, ctypes.byref(c), _ptr(src) if src.size else None, _ptr(copy), _ptr(st))
     return st
 
 

@@ -124,9 +124,12 @@ int reserve_patch(smol_csum_ctx_t* ctx, uint64_t n) {
 }
 
 int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t* b,
-        const smol_checksum_caps_t* caps, uint16_t* d_out, uint8_t* d_status, void* stream) {
+        const smol_checksum_caps_t* caps, uint16_t* d_out, uint8_t* d_status, void* stream,
+        const uint8_t* d_src = nullptr, const smol_csum_copy_t* d_copy = nullptr) {
     KParams p;
     std::memset(&p, 0, sizeof p);
+    p.src = d_src;
+    p.copy = d_copy;
     p.buf = d_buf;
     p.desc = b->desc;
     p.n = b->n;
@@ -156,6 +159,11 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     if (mode == MODE_DATA && variant > 2) variant = 0;
     const bool use_tile = variant >= 3;
     const hipStream_t s = (hipStream_t)stream;
+    if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
+        hipError_t e = launch_csum(MODE_COPY, shape, 1, p, ctx->max_blocks, s);
+        if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
+        return SMOL_OK;
+    }
     if (use_tile && !(mode == MODE_EMIT && ctx->defer_emit)) {
         hipError_t e = launch_tile(mode, shape, variant - 3, ctx->tile_records, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
@@ -330,6 +338,16 @@ int smol_csum_batch_verify(smol_csum_ctx_t* ctx, const uint8_t* d_buf, const smo
     if (rc != SMOL_OK || b->n == 0) return rc;
     if (!d_status) return SMOL_EINVAL;
     return run(ctx, MODE_VERIFY, const_cast<uint8_t*>(d_buf), b, caps, nullptr, d_status, stream);
+}
+
+int smol_csum_batch_copy_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* b,
+                              const uint8_t* d_src, const smol_csum_copy_t* d_copy,
+                              const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream) {
+    if (!ctx || !caps_valid(caps)) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK || b->n == 0) return rc;
+    if (!d_src || !d_copy || ((uintptr_t)d_copy & 15u) != 0) return SMOL_EINVAL;
+    return run(ctx, MODE_COPY, d_buf, b, caps, nullptr, d_status, stream, d_src, d_copy);
 }
 
 const char* smol_csum_last_error(void) { return g_last_error.c_str(); }

@@ -49,10 +49,16 @@ typedef GMEM uint16_t* gu16;
 struct RecRef {
     uint64_t a0;  // absolute address of the record's first byte
     uint32_t len;
-    uint32_t kind;
+    uint32_t kind;  // SMOL_KIND_*; MODE_COPY adds KIND_BAD_COPY for a copy range that does not fit
+    // MODE_COPY only: the record's payload [p0, p1) comes from sb + offset (sb = source address of
+    // record offset 0, i.e. src + src_offset - dst_offset)
+    uint64_t sb;
+    uint32_t p0, p1;
 };
 
-template <bool IMPLICIT>
+constexpr uint32_t KIND_BAD_COPY = 0x100;
+
+template <bool IMPLICIT, bool COPY>
 __device__ __forceinline__ RecRef rec_at(const KParams& p, uint64_t r) {
     RecRef rr;
     if (IMPLICIT) {
@@ -64,6 +70,19 @@ __device__ __forceinline__ RecRef rec_at(const KParams& p, uint64_t r) {
         rr.a0 = (uint64_t)p.buf + ((uint64_t)d.x | ((uint64_t)d.y << 32));
         rr.len = d.z;
         rr.kind = d.w & 0xffu;
+    }
+    rr.sb = 0;
+    rr.p0 = rr.p1 = 0;
+    if (COPY) {
+        const u32x4 c = *(gcv4)((uint64_t)p.copy + 16 * r);
+        const uint64_t so = (uint64_t)c.x | ((uint64_t)c.y << 32);
+        if ((uint64_t)c.z + c.w <= rr.len) {
+            rr.p0 = c.z;
+            rr.p1 = c.z + c.w;
+            rr.sb = (uint64_t)p.src + so - c.z;
+        } else {
+            rr.kind |= KIND_BAD_COPY;
+        }
     }
     return rr;
 }
@@ -79,19 +98,67 @@ __device__ __forceinline__ u32x4 ld16(gcv4 q) {
     return *q;
 }
 
+// The registers of one step: U record chunks; MODE_COPY adds the two aligned source chunks that
+// cover each destination chunk's payload bytes.
+template <int U, bool COPY>
+struct Regs {
+    u32x4 v[U];
+};
+template <int U>
+struct Regs<U, true> {
+    u32x4 v[U], s0[U], s1[U];
+};
+
 // Issue the U loads of one step.  Unconditional: chunks past the record (or a step that does
-// not exist) read the dummy line instead.
-template <int G, int U, bool NT>
-__device__ __forceinline__ void load_step(u32x4 (&v)[U], const RecRef& rr, uint32_t nch,
+// not exist) read the dummy line instead.  MODE_COPY: chunks entirely inside the payload are not
+// read from the record (they are replaced), and the source chunks are read only where they hold
+// payload bytes (so no load ever leaves the source range's aligned chunks).
+template <int G, int U, bool NT, bool COPY>
+__device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, uint32_t nch,
                                           uint32_t step, int lane, bool valid, uint64_t dummy) {
     const uint64_t base = rr.a0 & ~15ull;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t k = step * (G * U) + u * G + lane;
-        const uint64_t a = (valid && k < nch) ? base + 16ull * k : dummy;
-        v[u] = ld16<NT>((gcv4)a);
+        const bool in = valid && k < nch;
+        if constexpr (!COPY) {
+            R.v[u] = ld16<NT>((gcv4)(in ? base + 16ull * k : dummy));
+        } else {
+            const int64_t pos = (int64_t)(16u * k) - (int64_t)(rr.a0 & 15u);  // record offset of the chunk
+            const bool full = pos >= (int64_t)rr.p0 && pos + 16 <= (int64_t)rr.p1;
+            const bool pay = rr.p1 > rr.p0 && pos < (int64_t)rr.p1 && pos + 16 > (int64_t)rr.p0;
+            R.v[u] = ld16<NT>((gcv4)(in && !full ? base + 16ull * k : dummy));
+            const uint64_t sa = rr.sb + (uint64_t)pos;                 // source of the chunk's byte 0
+            const uint64_t sA = sa & ~15ull;
+            const uint64_t first = (rr.sb + rr.p0) & ~15ull;           // first / last aligned source
+            const uint64_t last = (rr.sb + rr.p1 - 1) & ~15ull;        // chunks holding payload
+            R.s0[u] = ld16<NT>((gcv4)(in && pay && sA >= first ? sA : dummy));
+            R.s1[u] = ld16<NT>((gcv4)(in && pay && (sa & 15u) && sA + 16 <= last ? sA + 16 : dummy));
+        }
     }
 }
+
+// Bytes sh .. sh+15 of the 32-byte pair (lo, hi), sh in [0, 16).
+__device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint32_t sh) {
+    const uint32_t q = sh >> 2, b = sh & 3u;
+    auto pick = [&](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+        return q == 0 ? a0 : q == 1 ? a1 : q == 2 ? a2 : a3;
+    };
+    const uint32_t x0 = pick(lo.x, lo.y, lo.z, lo.w);
+    const uint32_t x1 = pick(lo.y, lo.z, lo.w, hi.x);
+    const uint32_t x2 = pick(lo.z, lo.w, hi.x, hi.y);
+    const uint32_t x3 = pick(lo.w, hi.x, hi.y, hi.z);
+    const uint32_t x4 = pick(hi.x, hi.y, hi.z, hi.w);
+    u32x4 r;
+    r.x = __builtin_amdgcn_alignbyte(x1, x0, b);
+    r.y = __builtin_amdgcn_alignbyte(x2, x1, b);
+    r.z = __builtin_amdgcn_alignbyte(x3, x2, b);
+    r.w = __builtin_amdgcn_alignbyte(x4, x3, b);
+    return r;
+}
+
+// Byte mask of dword i (bytes 4i .. 4i+3 of a chunk) for chunk-relative byte range [lo, hi).
+__device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int i) { return mask_dword(0xffffffffu, lo - 4 * i, hi - 4 * i); }
 
 // One byte from global memory, waited for inside the asm statement.  Used only for header bytes
 // outside the LDS window (behind a long IPv6 Hop-by-Hop header).  Hidden from the compiler on
@@ -156,13 +223,18 @@ struct Walk {
     Geom g;          // cur's geometry (protocol modes)
     int s1;          // end of the summed span, relative to the record start
     uint32_t acc, acc2;
+    uint32_t fip, fl4;  // MODE_COPY: record offsets of the fields emit writes (NO_FIELD if none)
 };
+
+constexpr uint32_t NO_FIELD = 0x3fffffffu;
 
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF>
-__device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)[U], u32x4 (&nx)[U],
-                                          int lane, uint64_t ngroups, u32x4* win) {
+__device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
+                                          Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win) {
+    constexpr bool COPY = MODE == MODE_COPY;
+    constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
     const uint8_t* winb = reinterpret_cast<const uint8_t*>(win);
     const uint32_t nsteps = w.nch == 0 ? 1u : (w.nch + (G * U) - 1) / (G * U);
     const bool last = w.step + 1 >= nsteps;
@@ -171,12 +243,12 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
     const RecRef rec2 = last ? w.nxt : w.cur;
     const uint32_t nch2 = last ? n_chunks(w.nxt) : w.nch;
     const uint32_t step2 = last ? 0u : w.step + 1;
-    if (PF) load_step<G, U, NT>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
+    if (PF) load_step<G, U, NT, COPY>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
         const uint64_t r3 = r2 + ngroups < p.n ? r2 + ngroups : p.n - 1;
-        const RecRef t = rec_at<IMPLICIT>(p, r3);
+        const RecRef t = rec_at<IMPLICIT, COPY>(p, r3);
         if (last) nxt2 = t;
     }
 
@@ -184,19 +256,85 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
     // record byte o: LDS window when inside it, else global memory (long IPv6 extension chains)
     auto rd = [&](uint32_t o) -> uint32_t {
         const uint32_t x = head + o;
-        return x < (uint32_t)WIN_BYTES ? (uint32_t)winb[x] : ld_byte_sync(w.cur.a0 + o);
+        if (x < (uint32_t)WIN_BYTES) return (uint32_t)winb[x];
+        if (COPY && o >= w.cur.p0 && o < w.cur.p1) return ld_byte_sync(w.cur.sb + o);
+        return ld_byte_sync(w.cur.a0 + o);
     };
+    // MODE_COPY: this step's chunks with the payload merged in (and stored once the fields are known)
+    u32x4 cm[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cm[u] = cv.v[u];
+    if constexpr (COPY) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = w.step * (G * U) + u * G + lane;
+            const int pos = (int)(16u * k) - (int)head;
+            const int lo = (int)w.cur.p0 - pos, hi = (int)w.cur.p1 - pos;
+            if (k < w.nch && w.cur.p1 > w.cur.p0 && hi > 0 && lo < 16) {
+                const uint64_t sa = w.cur.sb + (uint64_t)(int64_t)pos;
+                const u32x4 src = funnel16(cv.s0[u], cv.s1[u], (uint32_t)(sa & 15u));
+                const uint32_t m0 = byte_mask(lo, hi, 0), m1 = byte_mask(lo, hi, 1);
+                const uint32_t m2 = byte_mask(lo, hi, 2), m3 = byte_mask(lo, hi, 3);
+                cm[u].x = (src.x & m0) | (cm[u].x & ~m0);
+                cm[u].y = (src.y & m1) | (cm[u].y & ~m1);
+                cm[u].z = (src.z & m2) | (cm[u].z & ~m2);
+                cm[u].w = (src.w & m3) | (cm[u].w & ~m3);
+            }
+        }
+    }
     if (w.step == 0) {
         w.acc = 0;
         w.acc2 = 0;
         if (MODE == MODE_DATA) {
             w.s1 = (int)w.cur.len;
         } else {
-            if (lane < WIN_BYTES / 16 && (uint32_t)lane < w.nch) win[lane] = cv[0];
+            if (lane < WIN_BYTES / 16 && (uint32_t)lane < w.nch) win[lane] = cm[0];
             wave_lds_sync();
-            w.g = parse_geometry(rd, w.cur.len, w.cur.kind);
+            if (COPY && (w.cur.kind & KIND_BAD_COPY)) {
+                w.g = Geom{};
+                w.g.st = SMOL_ST_MALFORMED;  // copy range does not fit: record left untouched
+            } else {
+                w.g = parse_geometry(rd, w.cur.len, w.cur.kind);
+            }
             // the lanes sum [0, span_end): the header part is subtracted at the end
             w.s1 = (w.g.proto != P_NONE && !(w.g.st & SMOL_ST_MALFORMED)) ? (int)w.g.span_end : 0;
+            if (COPY) {
+                w.fip = w.g.fam == 4 ? w.g.ip_off + 10 : NO_FIELD;
+                w.fl4 = (w.g.proto != P_NONE && !(w.g.st & SMOL_ST_MALFORMED)) ? w.g.l4_off + w.g.fo : NO_FIELD;
+            }
+        }
+    }
+    if constexpr (COPY) {  // store the payload bytes of this step (all of them, summed or not)
+        const gu8 base = (gu8)(w.cur.a0 & ~15ull);
+        const int f0b = (int)w.fip, f1b = (int)w.fl4;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = w.step * (G * U) + u * G + lane;
+            const int pos = (int)(16u * k) - (int)head;
+            const int lo = (int)w.cur.p0 - pos, hi = (int)w.cur.p1 - pos;
+            if (k < w.nch && w.cur.p1 > w.cur.p0 && hi > 0 && lo < 16) {
+                const int f0 = f0b - pos, f1 = f1b - pos;
+                const bool field = (f0 > -2 && f0 < 16) || (f1 > -2 && f1 < 16);
+                const gu8 dst = base + 16u * k;
+                if (lo <= 0 && hi >= 16 && !field) {
+                    *(GMEM u32x4*)dst = cm[u];
+                } else {
+                    const uint32_t cw[4] = {cm[u].x, cm[u].y, cm[u].z, cm[u].w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        uint32_t keep = byte_mask(lo, hi, i);
+                        keep &= ~byte_mask(f0, f0 + 2, i);
+                        keep &= ~byte_mask(f1, f1 + 2, i);
+                        if (keep == 0xffffffffu) {
+                            *(GMEM uint32_t*)(dst + 4 * i) = cw[i];
+                        } else if (keep) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (keep & (0xffu << (8 * j))) dst[4 * i + j] = (uint8_t)(cw[i] >> (8 * j));
+                        }
+                    }
+                }
+            }
         }
     }
 
@@ -207,7 +345,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
         const uint32_t k = w.step * (G * U) + u * G + lane;
         const int pos = (int)(16u * k) - (int)head;  // chunk start relative to the record
         if (k < w.nch && pos < s1) {
-            const u32x4 c = cv[u];
+            const u32x4 c = cm[u];
             if (pos < 0 || pos + 16 > s1) {  // first chunk (bytes before the record) / tail
                 if (MODE == MODE_DATA) {
                     const int lo = -pos, hi = s1 - pos;
@@ -255,7 +393,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
             if (g.fam == 4) {
                 for (uint32_t i = lane; i < g.ip_hl / 2; i += G) {
                     const uint32_t o = head + g.ip_off + 2 * i;
-                    if (!(MODE == MODE_EMIT && i == 5)) hsum += (winb[o] << 8) | winb[o + 1];
+                    if (!(EMITS && i == 5)) hsum += (winb[o] << 8) | winb[o + 1];
                 }
             }
             if (l4 && (g.proto == P_UDP || g.proto == P_TCP || g.proto == P_ICMP6)) {
@@ -277,7 +415,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
                 uint64_t patch = 0;  // emit: the field writes of this record (see PATCH_* below)
                 if (g.fam == 4) {
                     const uint32_t hdr = fold32(hsum);
-                    if (MODE == MODE_EMIT) {
+                    if (EMITS) {
                         const uint32_t v = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
                         patch |= (uint64_t)v | PATCH_IP | (g.ip_off ? PATCH_ETH : 0ull);
                     } else {
@@ -292,7 +430,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
                     // aligned-word sum of the L4 span = lanes' sum of [0, span_end) minus the
                     // header bytes [0, l4_off) (exact: no u32 wrap below 131072 bytes)
                     uint32_t s = tot - pre;
-                    if (MODE == MODE_EMIT) {
+                    if (EMITS) {
                         // the reference zeroes the field before summing: remove its bytes (the
                         // field offset is even: its parity is the record start's)
                         const uint32_t f0 = field >> 8, f1 = field & 0xffu;
@@ -314,7 +452,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
                         case P_ICMP6: gate_caps = p.caps_icmpv6; break;
                         default: gate_caps = SMOL_CHECKSUM_NONE; break;  // IGMP
                     }
-                    if (MODE == MODE_EMIT) {
+                    if (EMITS) {
                         const bool fill = g.proto == P_IGMP ? true : caps_tx(gate_caps);
                         uint32_t c = ~comb & 0xffffu;
                         if (g.proto == P_UDP && c == 0) c = 0xffffu;  // udp.rs:207
@@ -326,8 +464,8 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
                         l4_ok = caps_rx(gate_caps) ? l4_valid : 1u;
                     }
                 }
-                if (MODE == MODE_EMIT) {
-                    if (p.patch) {
+                if (EMITS) {
+                    if (!COPY && p.patch) {
                         // deferred: the scatter pass writes the fields after every read is done
                         ((GMEM uint64_t*)p.patch)[r] = patch;
                     } else {
@@ -358,12 +496,14 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, u32x4 (&cv)
 }
 
 // MODE_DATA: checksum::data over [0, len).  MODE_EMIT / MODE_VERIFY: the protocol gates.
-// VAR: 0 = non-temporal loads + register prefetch (default), 1 = plain loads + prefetch,
+// MODE_COPY: payload copy + emit in one pass.
+// VAR: 0 = non-temporal loads + register prefetch, 1 = plain loads + prefetch (default),
 // 2 = non-temporal loads, no prefetch (each step loads then waits; occupancy hides latency).
 template <int G, int U, int MODE, bool IMPLICIT, int VAR>
 __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool NT = VAR != 1;
     constexpr bool PF = VAR != 2;
+    constexpr bool COPY = MODE == MODE_COPY;
     constexpr int GPB = 256 / G;
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     __shared__ u32x4 win[GPB][WIN_BYTES / 16];
@@ -374,18 +514,19 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     Walk w;
     w.r = (uint64_t)blockIdx.x * GPB + gib;
     if (w.r >= p.n) return;
-    w.cur = rec_at<IMPLICIT>(p, w.r);
-    w.nxt = rec_at<IMPLICIT>(p, w.r + ngroups < p.n ? w.r + ngroups : p.n - 1);
+    w.cur = rec_at<IMPLICIT, COPY>(p, w.r);
+    w.nxt = rec_at<IMPLICIT, COPY>(p, w.r + ngroups < p.n ? w.r + ngroups : p.n - 1);
     w.nch = n_chunks(w.cur);
     w.step = 0;
     w.g = Geom{};
     w.s1 = 0;
     w.acc = w.acc2 = 0;
+    w.fip = w.fl4 = NO_FIELD;
 
-    u32x4 va[U];
+    Regs<U, COPY> va;
     if (PF) {
-        u32x4 vb[U];
-        load_step<G, U, NT>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
+        Regs<U, COPY> vb;
+        load_step<G, U, NT, COPY>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
             if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, vb, lane, ngroups, &win[gib][0])) break;
@@ -393,7 +534,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
         }
     } else {
         while (true) {
-            load_step<G, U, NT>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy);
+            load_step<G, U, NT, COPY>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy);
             if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, va, lane, ngroups, &win[gib][0])) break;
         }
     }
@@ -471,10 +612,27 @@ static hipError_t launch_mode(int shape, int var, const KParams& p, uint32_t max
     }
 }
 
+// MODE_COPY keeps three chunks per lane and step (record + two source chunks), so it is built for
+// the U <= 3 shapes only (wider shapes map to the same group size with fewer chunks) and for the
+// plain-load variant (measured best for emit).
+template <bool IMPLICIT>
+static hipError_t launch_copy(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    switch (shape) {
+        case CFG_G8U6: return launch_one<8, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
+        case CFG_G32U3:
+        case CFG_G32U4: return launch_one<32, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
+        case CFG_G64U2:
+        case CFG_G64U4: return launch_one<64, 2, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
+        default: return launch_one<16, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
+    }
+}
+
 hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (mode) {
         case MODE_DATA: return launch_mode<MODE_DATA>(shape, var, p, max_blocks, s);
         case MODE_EMIT: return launch_mode<MODE_EMIT>(shape, var, p, max_blocks, s);
+        case MODE_COPY:
+            return p.desc == nullptr ? launch_copy<true>(shape, p, max_blocks, s) : launch_copy<false>(shape, p, max_blocks, s);
         default: return launch_mode<MODE_VERIFY>(shape, var, p, max_blocks, s);
     }
 }

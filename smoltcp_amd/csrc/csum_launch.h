@@ -9,7 +9,7 @@
 
 namespace smolcsum {
 
-enum { MODE_DATA = 0, MODE_EMIT = 1, MODE_VERIFY = 2 };
+enum { MODE_DATA = 0, MODE_EMIT = 1, MODE_VERIFY = 2, MODE_COPY = 3 };  // COPY: fused copy + emit
 
 // Launch shapes: lanes per record (G) x 16-byte chunks per lane per step (U).
 enum {
@@ -36,6 +36,8 @@ struct KParams {
     const uint8_t* dummy;  // 16-byte-aligned device line read by loads that have nothing to read
     uint64_t* patch;       // MODE_EMIT: deferred field writes (one u64 per record) or nullptr
     uint32_t num_cu;       // compute units of the device (grid sizing)
+    const uint8_t* src;             // MODE_COPY: payload source buffer
+    const smol_csum_copy_t* copy;   // MODE_COPY: one payload copy per record (16-B aligned)
 };
 
 // Workgroups of `kernel` (256 threads) resident on the whole device, capped at max_blocks.

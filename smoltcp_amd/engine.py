@@ -36,6 +36,20 @@ DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("kind", "u1"), ("flag
                        ("reserved", "<u2")])
 assert DESC_DTYPE.itemsize == 16
 
+# smol_csum_copy_t: one payload copy per record (smol_csum_batch_copy_emit)
+COPY_DTYPE = np.dtype([("src_offset", "<u8"), ("dst_offset", "<u4"), ("len", "<u4")])
+assert COPY_DTYPE.itemsize == 16
+
+
+def make_copies(src_offsets, dst_offsets, lengths) -> np.ndarray:
+    """Host array of smol_csum_copy_t (view it as uint8 and copy it to the device)."""
+    n = len(src_offsets)
+    c = np.zeros(n, dtype=COPY_DTYPE)
+    c["src_offset"] = np.asarray(src_offsets, dtype=np.uint64)
+    c["dst_offset"] = np.broadcast_to(np.asarray(dst_offsets, dtype=np.uint32), (n,))
+    c["len"] = np.broadcast_to(np.asarray(lengths, dtype=np.uint32), (n,))
+    return c
+
 
 def make_descriptors(offsets, lengths, kinds) -> np.ndarray:
     """Host array of smol_csum_desc_t (view it as uint8 and copy it to the device)."""
@@ -145,6 +159,19 @@ class ChecksumEngine:
         check(lib().smol_csum_batch_emit(self._h, buf.data_ptr(), ctypes.byref(b), ctypes.byref(c),
                                          status.data_ptr() if status is not None else None,
                                          self._stream(stream)), "smol_csum_batch_emit")
+        return status
+
+    def copy_emit(self, buf, batch: Batch, src, copies, caps=None, status=None, stream=None):
+        """Fused payload copy + emit (smol_csum_batch_copy_emit): ``copies`` is a device uint8
+        tensor of n smol_csum_copy_t (see make_copies), ``src`` the payload source tensor."""
+        self._check_buf(buf, batch)
+        assert src.is_cuda and copies.is_cuda and copies.numel() >= 16 * batch.n
+        b = batch.c()
+        c = _caps(caps)
+        check(lib().smol_csum_batch_copy_emit(self._h, buf.data_ptr(), ctypes.byref(b), src.data_ptr(),
+                                              copies.data_ptr(), ctypes.byref(c),
+                                              status.data_ptr() if status is not None else None,
+                                              self._stream(stream)), "smol_csum_batch_copy_emit")
         return status
 
     def verify(self, buf, batch: Batch, caps=None, status=None, stream=None):

@@ -172,6 +172,17 @@ public:
         check(smol_csum_batch_emit(ctx_, d_buf, &bc, &cc, d_status, stream), "smol_csum_batch_emit");
     }
 
+    // TcpRepr/UdpRepr::emit's "copy the payload, then fill": d_copy[i] moves record i's payload
+    // from d_src into the record, then the checksums are emitted, in one pass.
+    void copy_emit(uint8_t* d_buf, const Batch& b, const uint8_t* d_src, const smol_csum_copy_t* d_copy,
+                   const smoltcp::phy::ChecksumCapabilities& caps = {}, uint8_t* d_status = nullptr,
+                   void* stream = nullptr) {
+        auto bc = b.c();
+        auto cc = caps.c();
+        check(smol_csum_batch_copy_emit(ctx_, d_buf, &bc, d_src, d_copy, &cc, d_status, stream),
+              "smol_csum_batch_copy_emit");
+    }
+
     // Repr::parse checksum gates: d_status[i] = SMOL_ST_* bits.
     void verify(const uint8_t* d_buf, const Batch& b, uint8_t* d_status,
                 const smoltcp::phy::ChecksumCapabilities& caps = {}, void* stream = nullptr) {
