@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) void scatter_kernel(KParams p) {
 
 hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const uint64_t want = (p.n + 255) / 256;
-    const uint32_t blocks = (uint32_t)(want < max_blocks ? want : max_blocks);
+    const uint32_t blocks = grid_blocks(want, max_blocks);
     if (p.desc) hipLaunchKernelGGL(scatter_kernel<false>, dim3(blocks), dim3(256), 0, s, p);
     else hipLaunchKernelGGL(scatter_kernel<true>, dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
@@ -578,7 +578,7 @@ template <int G, int U, int MODE, bool IMPLICIT, int VAR>
 static hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
-    const uint32_t blocks = (uint32_t)(want < max_blocks ? want : max_blocks);
+    const uint32_t blocks = grid_blocks(want, max_blocks);
     hipLaunchKernelGGL((csum_kernel<G, U, MODE, IMPLICIT, VAR>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }

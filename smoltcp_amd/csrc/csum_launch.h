@@ -40,6 +40,16 @@ struct KParams {
     const smol_csum_copy_t* copy;   // MODE_COPY: one payload copy per record (16-B aligned)
 };
 
+// A dispatch may hold at most 2^32 - 1 work-items: 256-thread grids are capped at 2^24 - 1 blocks
+// (every kernel loops with a grid stride, so a capped grid still covers the whole batch; C5's 2^27
+// records per GPU need it).
+constexpr uint64_t kMaxGridBlocks = 0xFFFFFFull;
+__host__ __device__ inline uint32_t grid_blocks(uint64_t want, uint64_t cap) {
+    uint64_t b = want < cap ? want : cap;
+    b = b < kMaxGridBlocks ? b : kMaxGridBlocks;
+    return (uint32_t)(b ? b : 1);
+}
+
 // Workgroups of `kernel` (256 threads) resident on the whole device, capped at max_blocks.
 uint32_t resident_blocks(const void* kernel, uint32_t num_cu, uint32_t max_blocks);
 

@@ -364,7 +364,7 @@ static hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t 
     // An explicit cap (smol_csum_tool_set_max_blocks, num_cu == 0) makes the grid persistent.
     (void)kern;
     const uint64_t cap = p.num_cu == 0 ? max_blocks : (uint64_t)0x7fffffff;
-    const uint32_t blocks = (uint32_t)(want < cap ? want : cap);
+    const uint32_t blocks = grid_blocks(want, cap);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }

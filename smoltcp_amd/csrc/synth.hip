@@ -187,7 +187,7 @@ __global__ void corrupt_kernel(SynthParams p, uint32_t every) {
 
 hipError_t launch_synth(const SynthParams& p, uint32_t max_blocks, hipStream_t s) {
     const uint64_t want = (p.n + 3) / 4;
-    const uint32_t blocks = (uint32_t)(want < max_blocks ? want : max_blocks);
+    const uint32_t blocks = grid_blocks(want, max_blocks);
     hipLaunchKernelGGL(synth_kernel, dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }

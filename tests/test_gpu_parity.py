@@ -425,3 +425,20 @@ def test_empty_batch_and_errors(eng):
     eng.verify(buf, E.Batch.fixed(0, 0, 0))  # n == 0 is a no-op
     with pytest.raises(Exception):
         eng.verify(buf, E.Batch.fixed(1, 16, 16), caps=(9, 0, 0, 0, 0))
+
+
+def test_grid_cap_huge_batch(eng):
+    """2^27 records with 64-lane groups want more than 2^32 work-items: the launcher caps the grid
+    and the kernels' grid-stride loop still covers every record (C5 sizes)."""
+    rec = np.frombuffer(P.ipv4(V4A, V4B, 17, P.udp(1, 2, bytes(range(36)))), np.uint8)
+    buf = rec.copy()
+    oracle.batch_emit(buf, None, 1, 64, 64, 1)
+    d = torch.from_numpy(np.concatenate([buf, np.zeros(16, np.uint8)])).cuda()
+    n = 1 << 27
+    eng.set_shape(6)
+    try:
+        st = eng.verify(d, E.Batch.fixed(n, 0, len(rec), E.KIND_IP))
+    finally:
+        eng.set_shape(-1)
+    ref = oracle.batch_verify(buf.copy(), None, 1, 64, len(rec), 1)[0]
+    assert int((st == int(ref)).sum()) == n and (ref & E.ST_ACCEPT)

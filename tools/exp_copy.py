@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Time the fused copy + emit (C2copy workload) for every launch shape: one JSON line per shape."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from smoltcp_amd import engine as E  # noqa: E402
+
+
+def main():
+    n, L = 1 << 20, 1500
+    eng = E.ChecksumEngine(0)
+    dev = torch.device("cuda:0")
+    tx = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    b = E.Batch.fixed(n, L, L, E.KIND_IP)
+    eng.synth(tx, b, E.SYNTH_UDP4, 0x5EED0006)
+    src = torch.randint(0, 256, (n * 1472 + 16,), dtype=torch.uint8, device=dev)
+    cp = torch.from_numpy(E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472).view(np.uint8).copy()).to(dev)
+    for shape in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,3,5").split(",")]:
+        eng.set_shape(shape)
+        for _ in range(3):
+            eng.copy_emit(tx, b, src, cp)
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(20):
+            eng.copy_emit(tx, b, src, cp)
+        z.record()
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(z) / 20
+        moved = n * (28 + 1472 + 1472 + 4)
+        print(json.dumps({"shape": shape, "ms": round(ms, 4), "GBs_rw": round(moved / ms / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

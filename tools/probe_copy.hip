@@ -1,0 +1,91 @@
+// Copy-bandwidth probe: the read+write ceiling a fused copy + emit is measured against.
+// hipMemcpyAsync device-to-device and wave-contiguous copy kernels (plain / non-temporal).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+#define GMEM __attribute__((address_space(1)))
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int UNR, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void wave_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const uint64_t per = 64ull * UNR;
+    for (uint64_t base = w0 * per; base + per <= n16; base += nw * per) {
+        u32x4 v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const GMEM u32x4* q = (const GMEM u32x4*)(src + base + u * 64 + lane);
+            v[u] = NTL ? __builtin_nontemporal_load(q) : *q;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            GMEM u32x4* q = (GMEM u32x4*)(dst + base + u * 64 + lane);
+            if (NTS) __builtin_nontemporal_store(v[u], q); else *q = v[u];
+        }
+    }
+}
+
+// Strided copy like the C2 payloads: record r's 1472 B from src + r*1472 to dst + r*1500 + 28.
+__global__ __launch_bounds__(256) void rec_copy(const uint8_t* src, uint8_t* dst, uint64_t n) {
+    const int lane = threadIdx.x & 15;
+    const uint64_t ng = (uint64_t)gridDim.x * 16;
+    for (uint64_t r = (uint64_t)blockIdx.x * 16 + threadIdx.x / 16; r < n; r += ng) {
+        const GMEM uint32_t* s = (const GMEM uint32_t*)(src + r * 1472);
+        GMEM uint32_t* d = (GMEM uint32_t*)(dst + r * 1500 + 28);
+        for (int i = lane; i < 368; i += 16) d[i] = s[i];
+    }
+}
+
+// Same, but every byte of the destination records is written (the 28 header bytes too): no line
+// is left partially dirty.
+__global__ __launch_bounds__(256) void rec_copy_full(const uint8_t* src, uint8_t* dst, uint64_t n) {
+    const int lane = threadIdx.x & 15;
+    const uint64_t ng = (uint64_t)gridDim.x * 16;
+    for (uint64_t r = (uint64_t)blockIdx.x * 16 + threadIdx.x / 16; r < n; r += ng) {
+        const GMEM uint32_t* s = (const GMEM uint32_t*)(src + r * 1472);
+        GMEM uint32_t* d = (GMEM uint32_t*)(dst + r * 1500);
+        for (int i = lane; i < 375; i += 16) d[i] = i < 7 ? 0x01020304u : s[i - 7];
+    }
+}
+
+int main() {
+    const uint64_t bytes = 1500ull << 20;
+    uint8_t *a, *b;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes));
+    CK(hipMemset(a, 1, bytes));
+    CK(hipMemset(b, 2, bytes));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    auto timeit = [&](const char* name, auto fn) {
+        for (int i = 0; i < 3; ++i) fn();
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < 10; ++i) fn();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= 10;
+        printf("%-36s %8.4f ms  %7.1f GB/s (read+write)\n", name, ms, 2.0 * bytes / ms / 1e6);
+    };
+    const uint64_t n16 = bytes / 16;
+    timeit("hipMemcpyAsync D2D", [&] { CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0)); });
+    for (int bpc : {2, 4, 8}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "wave_copy U4 plain bpc=%d", bpc);
+        timeit(nm, [&] { hipLaunchKernelGGL((wave_copy<4, false, false>), dim3(256 * bpc), dim3(256), 0, 0, (const u32x4*)a, (u32x4*)b, n16); });
+        snprintf(nm, sizeof nm, "wave_copy U4 ntload bpc=%d", bpc);
+        timeit(nm, [&] { hipLaunchKernelGGL((wave_copy<4, true, false>), dim3(256 * bpc), dim3(256), 0, 0, (const u32x4*)a, (u32x4*)b, n16); });
+        snprintf(nm, sizeof nm, "wave_copy U4 nt both bpc=%d", bpc);
+        timeit(nm, [&] { hipLaunchKernelGGL((wave_copy<4, true, true>), dim3(256 * bpc), dim3(256), 0, 0, (const u32x4*)a, (u32x4*)b, n16); });
+        snprintf(nm, sizeof nm, "wave_copy U4 ntstore bpc=%d", bpc);
+        timeit(nm, [&] { hipLaunchKernelGGL((wave_copy<4, false, true>), dim3(256 * bpc), dim3(256), 0, 0, (const u32x4*)a, (u32x4*)b, n16); });
+    }
+    const uint64_t n = 1ull << 20;
+    timeit("rec_copy 1472 B -> stride 1500 (+28)", [&] { hipLaunchKernelGGL(rec_copy, dim3(256 * 8), dim3(256), 0, 0, a, b, n); });
+    timeit("rec_copy_full 1500 B (all bytes)", [&] { hipLaunchKernelGGL(rec_copy_full, dim3(256 * 8), dim3(256), 0, 0, a, b, n); });
+    CK(hipGetLastError());
+    return 0;
+}
