@@ -23,7 +23,7 @@ import os
 import re
 import shutil
 
-MODES = {"0": "data", "1": "emit", "2": "verify"}
+MODES = {"0": "data", "1": "emit", "2": "verify", "3": "copy_emit"}
 
 
 def _find(d, pattern):
