@@ -52,6 +52,11 @@ int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records);
 /* Emit as read pass + scatter pass, or (default) with the field stores inside the read pass. */
 int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int on);
 
+/* Fixed-stride emit writes each checksum field as the whole 64-B line(s) holding it, rebuilt from
+ * the record bytes just read (default on), instead of two 2-byte stores; a partial-line store makes
+ * HBM read the line back.  Off: always the 2-byte stores (A/B measurement). */
+int smol_csum_tool_set_line_writes(smol_csum_ctx_t* ctx, int on);
+
 /* Cap the number of workgroups per launch (0 = automatic: CUs x 8). */
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
 

@@ -30,7 +30,8 @@ ABI_SYMBOLS = [
 ]
 TOOL_SYMBOLS = [
     "smol_csum_tool_synth", "smol_csum_tool_corrupt", "smol_csum_tool_set_shape",
-    "smol_csum_tool_set_variant", "smol_csum_tool_set_deferred_emit", "smol_csum_tool_set_tile",
+    "smol_csum_tool_set_variant", "smol_csum_tool_set_deferred_emit", "smol_csum_tool_set_line_writes",
+    "smol_csum_tool_set_tile",
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
 ]
 
@@ -101,6 +102,8 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_ctx_reserve.restype = i32
     L.smol_csum_tool_set_deferred_emit.argtypes = [vp, i32]
     L.smol_csum_tool_set_deferred_emit.restype = i32
+    L.smol_csum_tool_set_line_writes.argtypes = [vp, i32]
+    L.smol_csum_tool_set_line_writes.restype = i32
     L.smol_csum_batch_data.argtypes = [vp, vp, ctypes.POINTER(BatchC), vp, vp]
     L.smol_csum_batch_data.restype = i32
     L.smol_csum_batch_emit.argtypes = [vp, vp, ctypes.POINTER(BatchC), ctypes.POINTER(Caps), vp, vp]

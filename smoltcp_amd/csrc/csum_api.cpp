@@ -27,6 +27,7 @@ struct smol_csum_ctx {
     uint64_t patch_cap;   // records the workspace holds
     int tile_records;     // tile kernel: records per wavefront tile (32 or 64)
     bool max_blocks_set;  // grid cap given explicitly (tooling)
+    bool line_writes;     // fixed-stride emit writes whole 64-B lines (default on; tooling can disable)
 };
 
 namespace smolcsum {
@@ -147,6 +148,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.status = d_status;
     p.dummy = ctx->dummy;
     p.num_cu = ctx->max_blocks_set ? 0u : (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);
+    p.linew = (mode == MODE_EMIT && !ctx->defer_emit && ctx->line_writes) ? 1u : 0u;
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
     int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr);
@@ -285,6 +287,7 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     c->defer_emit = false;
     c->tile_records = 32;
     c->max_blocks_set = false;
+    c->line_writes = true;
     c->patch = nullptr;
     c->patch_cap = 0;
     c->device = device;
@@ -401,6 +404,12 @@ int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records) {
 int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int on) {
     if (!ctx) return SMOL_EINVAL;
     ctx->defer_emit = on != 0;
+    return SMOL_OK;
+}
+
+int smol_csum_tool_set_line_writes(smol_csum_ctx_t* ctx, int on) {
+    if (!ctx) return SMOL_EINVAL;
+    ctx->line_writes = on != 0;
     return SMOL_OK;
 }
 

@@ -228,13 +228,71 @@ struct Walk {
 
 constexpr uint32_t NO_FIELD = 0x3fffffffu;
 
+// Emit line writes (fixed-stride emit, groups of <= 32 lanes).  A 2-byte field store is a
+// partial-line write: HBM reads the 64-B line back to merge it (tools/probe_wr.hip: full 64-B line
+// stores cost ~20 % less than two 2-B stores in the same line).  So the fields are written as the
+// whole 64-B line(s) that hold them, assembled from the LDS window (this record's first 128 B,
+// fields patched in) and, for the bytes before the record, from the previous record's last chunks,
+// which the neighbouring group of the same wavefront published in LDS at the same step.  Bytes of
+// another record are rewritten with the values just read, so a line write is used only when the
+// previous record (i) is adjacent (stride == len) and handled by this wavefront in this step,
+// (ii) has its last LW_TAIL chunks in LDS, and (iii) has no checksum field inside the line; the
+// line must also end inside this record and inside the window.  Otherwise the two 2-byte stores.
+template <int G, int MODE, bool IMPLICIT>
+struct LineWrites {
+    static constexpr bool value = MODE == MODE_EMIT && IMPLICIT && G <= 32;
+};
+constexpr uint32_t LW_TAIL = 5;  // chunks of a record's tail published for the next record
+
+template <int G>
+__device__ __forceinline__ void line_writes(const KParams& p, const Walk& w, int lane, int gib, u32x4* win,
+                                            const u32x4* tailw, const uint32_t* linfo, uint64_t patch_lane0) {
+    wave_lds_sync();
+    const uint32_t* me = linfo + gib * 4;
+    const uint64_t a0 = w.cur.a0;
+    const uint64_t base = a0 & ~15ull;
+    const uint32_t fip = me[2], fl4 = me[3];
+    const bool mine = me[0] == (uint32_t)w.r + 1u;  // this group published in this step
+    const bool any = mine && (fip != NO_FIELD || fl4 != NO_FIELD);
+    const uint64_t L1 = ((a0 + (fip != NO_FIELD ? fip : fl4)) & ~63ull);
+    const uint64_t L2 = ((a0 + (fl4 != NO_FIELD ? fl4 : fip)) & ~63ull);
+    // no 2-byte field may straddle a line boundary (odd strides): both bytes must be in the lines
+    bool ok = any && (gib % (64 / G)) != 0 && p.stride == p.len && w.r > 0 &&
+              (fip == NO_FIELD || ((a0 + fip) & 63u) != 63u) && (fl4 == NO_FIELD || ((a0 + fl4) & 63u) != 63u);
+    uint64_t tA = 0;
+    if (ok) {
+        const uint32_t* nb = linfo + (gib - 1) * 4;
+        const uint64_t a0p = a0 - p.stride;
+        const uint32_t nchp = (uint32_t)(((a0p + p.len + 15) >> 4) - (a0p >> 4));
+        tA = (a0p & ~15ull) + 16ull * (nchp - LW_TAIL);
+        ok = nb[0] == (uint32_t)(w.r - 1) + 1u && nb[1] != 0u && L1 >= tA && L2 + 64 <= a0 + p.len &&
+             L2 + 64 <= base + WIN_BYTES;
+        if (ok && nb[2] != NO_FIELD) ok = !(a0p + nb[2] + 2 > L1 && a0p + nb[2] < L2 + 64);
+        if (ok && nb[3] != NO_FIELD) ok = !(a0p + nb[3] + 2 > L1 && a0p + nb[3] < L2 + 64);
+    }
+    if (ok) {
+        const uint32_t nc = L2 == L1 ? 4u : 8u;
+        for (uint32_t c = (uint32_t)lane; c < nc; c += G) {
+            const uint64_t ca = (c < 4 ? L1 : L2) + 16ull * (c & 3u);
+            const u32x4 v = ca >= base ? win[(ca - base) >> 4] : tailw[(gib - 1) * LW_TAIL + ((ca - tA) >> 4)];
+            *(GMEM u32x4*)ca = v;
+        }
+    } else if (lane == 0 && any) {
+        const gu8 wrec = (gu8)a0;
+        if (fip != NO_FIELD) store_be16(wrec + fip, (uint32_t)(patch_lane0 & 0xffffu));
+        if (fl4 != NO_FIELD) store_be16(wrec + fl4, (uint32_t)((patch_lane0 >> 16) & 0xffffu));
+    }
+}
+
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
-                                          Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win) {
+                                          Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
+                                          int gib, u32x4* tailw, uint32_t* linfo) {
     constexpr bool COPY = MODE == MODE_COPY;
     constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
+    constexpr bool LW = LineWrites<G, MODE, IMPLICIT>::value;
     const uint8_t* winb = reinterpret_cast<const uint8_t*>(win);
     const uint32_t nsteps = w.nch == 0 ? 1u : (w.nch + (G * U) - 1) / (G * U);
     const bool last = w.step + 1 >= nsteps;
@@ -370,6 +428,16 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     if (last) {
         const bool odd = (w.cur.a0 & 1u) != 0;
         const uint64_t r = w.r;
+        const bool lw = LW && p.linew;
+        if constexpr (LW) {
+            if (lw) {  // the record's last LW_TAIL chunks, for the next record's line writes
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t k = w.step * (G * U) + u * G + lane;
+                    if (k < w.nch && k + LW_TAIL >= w.nch) tailw[gib * LW_TAIL + (k + LW_TAIL - w.nch)] = cm[u];
+                }
+            }
+        }
         if (MODE == MODE_DATA) {
             // exact little-endian word sum relative to the span start, modulo 2^32
             const uint32_t s_rel = odd ? (w.acc2 + (w.acc << 8)) : (w.acc + (w.acc2 << 8));
@@ -406,13 +474,12 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             pre = group_sum<G>(pre);
             hsum = group_sum<G>(hsum);
             psum = group_sum<G>(psum);
+            uint64_t patch = 0;  // emit: the field writes of this record (see PATCH_* below)
+            const gu8 wrec = (gu8)w.cur.a0;
             if (lane == 0) {
-                const gu8 wrec = (gu8)w.cur.a0;
-                (void)wrec;
                 uint32_t st = g.st;
                 // IPv4 header: data(header) (canonical fold of the big-endian word sum)
                 uint32_t ip_valid = 1, ip_ok = 1;
-                uint64_t patch = 0;  // emit: the field writes of this record (see PATCH_* below)
                 if (g.fam == 4) {
                     const uint32_t hdr = fold32(hsum);
                     if (EMITS) {
@@ -468,9 +535,27 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                     if (!COPY && p.patch) {
                         // deferred: the scatter pass writes the fields after every read is done
                         ((GMEM uint64_t*)p.patch)[r] = patch;
-                    } else {
+                    } else if (!lw) {
                         if (patch & PATCH_IP) store_be16(wrec + g.ip_off + 10, (uint32_t)(patch & 0xffffu));
                         if (patch & PATCH_L4) store_be16(wrec + ((patch >> 32) & 0xffffffu), (uint32_t)((patch >> 16) & 0xffffu));
+                    } else {
+                        // line writes: publish the fields and patch them into the LDS window
+                        uint8_t* wb = reinterpret_cast<uint8_t*>(win);
+                        const uint32_t fip = (patch & PATCH_IP) ? g.ip_off + 10 : NO_FIELD;
+                        const uint32_t fl4 = (patch & PATCH_L4) ? (uint32_t)((patch >> 32) & 0xffffffu) : NO_FIELD;
+                        if (fip != NO_FIELD && head + fip + 1 < (uint32_t)WIN_BYTES) {
+                            wb[head + fip] = (uint8_t)(patch >> 8);
+                            wb[head + fip + 1] = (uint8_t)patch;
+                        }
+                        if (fl4 != NO_FIELD && head + fl4 + 1 < (uint32_t)WIN_BYTES) {
+                            wb[head + fl4] = (uint8_t)(patch >> 24);
+                            wb[head + fl4 + 1] = (uint8_t)(patch >> 16);
+                        }
+                        const bool tail_ok = w.nch >= LW_TAIL && (w.nch - LW_TAIL) >= w.step * (G * U);
+                        linfo[gib * 4 + 0] = (uint32_t)r + 1u;
+                        linfo[gib * 4 + 1] = tail_ok ? 1u : 0u;
+                        linfo[gib * 4 + 2] = fip;
+                        linfo[gib * 4 + 3] = fl4;
                     }
                     if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
                 } else {
@@ -481,6 +566,9 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                           ((ip_ok && l4_ok && !mal) ? SMOL_ST_ACCEPT : 0u);
                     ((gu8)p.status)[r] = (uint8_t)st;
                 }
+            }
+            if constexpr (LW) {
+                if (lw) line_writes<G>(p, w, lane, gib, win, tailw, linfo, patch);
             }
         }
     }
@@ -507,6 +595,9 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr int GPB = 256 / G;
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     __shared__ u32x4 win[GPB][WIN_BYTES / 16];
+    constexpr bool LW = LineWrites<G, MODE, IMPLICIT>::value;
+    __shared__ u32x4 tailw[LW ? GPB * LW_TAIL : 1];
+    __shared__ uint32_t linfo[LW ? GPB * 4 : 1];
 
     const int lane = (int)(threadIdx.x % G);
     const int gib = (int)(threadIdx.x / G);
@@ -522,6 +613,9 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     w.s1 = 0;
     w.acc = w.acc2 = 0;
     w.fip = w.fl4 = NO_FIELD;
+    if (LW) {
+        for (int i = lane; i < 4; i += G) linfo[gib * 4 + i] = 0u;
+    }
 
     Regs<U, COPY> va;
     if (PF) {
@@ -529,13 +623,13 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
         load_step<G, U, NT, COPY>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, vb, lane, ngroups, &win[gib][0])) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, vb, va, lane, ngroups, &win[gib][0])) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
         }
     } else {
         while (true) {
             load_step<G, U, NT, COPY>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy);
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, va, lane, ngroups, &win[gib][0])) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, va, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
         }
     }
 }

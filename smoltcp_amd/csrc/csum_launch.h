@@ -38,6 +38,7 @@ struct KParams {
     uint32_t num_cu;       // compute units of the device (grid sizing)
     const uint8_t* src;             // MODE_COPY: payload source buffer
     const smol_csum_copy_t* copy;   // MODE_COPY: one payload copy per record (16-B aligned)
+    uint32_t linew;                 // MODE_EMIT, fixed stride: write whole 64-B lines (see csum_kernels.hip)
 };
 
 // A dispatch may hold at most 2^32 - 1 work-items: 256-thread grids are capped at 2^24 - 1 blocks

@@ -219,6 +219,9 @@ class ChecksumEngine:
         check(lib().smol_csum_tool_set_deferred_emit(self._h, int(bool(on))),
               "smol_csum_tool_set_deferred_emit")
 
+    def set_line_writes(self, on: bool):
+        check(lib().smol_csum_tool_set_line_writes(self._h, int(bool(on))), "smol_csum_tool_set_line_writes")
+
     def reserve(self, max_records: int):
         check(lib().smol_csum_ctx_reserve(self._h, int(max_records)), "smol_csum_ctx_reserve")
 

@@ -442,3 +442,38 @@ def test_grid_cap_huge_batch(eng):
         eng.set_shape(-1)
     ref = oracle.batch_verify(buf.copy(), None, 1, 64, len(rec), 1)[0]
     assert int((st == int(ref)).sum()) == n and (ref & E.ST_ACCEPT)
+
+
+@pytest.mark.parametrize("profile,kind", [(E.SYNTH_UDP4, E.KIND_IP), (E.SYNTH_TCP4, E.KIND_IP),
+                                          (E.SYNTH_V6MIX, E.KIND_IP), (E.SYNTH_ETH_TCP4, E.KIND_ETH)])
+def test_emit_line_writes_match_oracle(eng, profile, kind):
+    """Fixed-stride emit with whole-line field writes (default) against the oracle over the whole
+    buffer (bytes of neighbouring records are rewritten by line writes and must not change):
+    strides short enough that neighbouring fields share lines, odd strides, every shape, a
+    persistent grid (several records per group), caps that write zero fields."""
+    for stride in (64, 66, 80, 97, 128, 200, 1500, 1501, 1519):
+        n = 1031
+        buf = torch.zeros(n * stride + 64, dtype=torch.uint8, device="cuda:0")
+        batch = E.Batch.fixed(n, stride, stride, kind)
+        eng.synth(buf, batch, profile, seed=stride * 13 + profile)
+        host = buf.cpu().numpy().copy()
+        for shape, blocks, caps in [(-1, 0, (0, 0, 0, 0, 0)), (0, 3, (0, 0, 0, 0, 0)), (1, 0, (2, 3, 0, 1, 0)),
+                                    (3, 0, (0, 0, 0, 0, 0)), (4, 5, (3, 2, 2, 3, 3))]:
+            for lw in (True, False):
+                eng.set_shape(shape)
+                eng.set_max_blocks(blocks)
+                eng.set_line_writes(lw)
+                try:
+                    d = torch.from_numpy(host.copy()).cuda()
+                    st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+                    eng.emit(d, batch, caps=caps, status=st)
+                    got = d.cpu().numpy()
+                finally:
+                    eng.set_shape(-1)
+                    eng.set_max_blocks(0)
+                    eng.set_line_writes(True)
+                ref = host.copy()
+                ref_st = oracle.batch_emit(ref, None, n, stride, stride, kind, caps)
+                diff = np.nonzero(got != ref)[0]
+                assert diff.size == 0, (profile, stride, shape, blocks, caps, lw, diff[:8])
+                assert np.array_equal(st.cpu().numpy(), ref_st)
