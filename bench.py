@@ -45,6 +45,7 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
     ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
+    ap.add_argument("--variant", type=int, default=-1, help="force a kernel variant (tuning)")
     ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
     return ap.parse_args()
 
@@ -233,6 +234,8 @@ def main():
     eng = E.ChecksumEngine(local)
     if args.shape >= 0:
         eng.set_shape(args.shape)
+    if args.variant >= 0:
+        eng.set_variant(args.variant)
     wl = Workload(E, eng, args.config, args.n, rank, dev)
     torch.cuda.synchronize()
 

@@ -477,3 +477,42 @@ def test_emit_line_writes_match_oracle(eng, profile, kind):
                 diff = np.nonzero(got != ref)[0]
                 assert diff.size == 0, (profile, stride, shape, blocks, caps, lw, diff[:8])
                 assert np.array_equal(st.cpu().numpy(), ref_st)
+
+
+@pytest.mark.parametrize("variant", [0, 2, 3, 4])
+def test_variants_fixed_stride(eng, variant):
+    """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
+    the oracle on fixed-stride batches: strides equal to the record length (neighbours share
+    lines), odd strides, gaps, every shape, natural and persistent grids."""
+    for profile, kind, L in [(E.SYNTH_UDP4, E.KIND_IP, 1500), (E.SYNTH_V6MIX, E.KIND_IP, 1320),
+                             (E.SYNTH_TCP4, E.KIND_IP, 97), (E.SYNTH_ETH_TCP4, E.KIND_ETH, 1514),
+                             (E.SYNTH_UDP4, E.KIND_IP, 128), (E.SYNTH_TCP4, E.KIND_IP, 4000)]:
+        for stride in (L, L + 1, L + 16):
+            n = 1029
+            buf = torch.zeros(n * stride + 64, dtype=torch.uint8, device="cuda:0")
+            batch = E.Batch.fixed(n, stride, L, kind)
+            eng.synth(buf, batch, profile, seed=L + stride + variant)
+            eng.emit(buf, batch)
+            eng.corrupt(buf, batch, every=7, seed=L)
+            host = buf.cpu().numpy().copy()
+            ref_v = oracle.batch_verify(host.copy(), None, n, stride, L, kind, CAPS_DEFAULT)
+            ref_e = host.copy()
+            ref_es = oracle.batch_emit(ref_e, None, n, stride, L, kind, CAPS_DEFAULT)
+            for shape in SHAPES:
+                for blocks in (0, 7):
+                    eng.set_variant(variant)
+                    eng.set_shape(shape)
+                    eng.set_max_blocks(blocks)
+                    try:
+                        st = eng.verify(buf, batch).cpu().numpy()
+                        d2 = buf.clone()
+                        est = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+                        eng.emit(d2, batch, status=est)
+                        got = d2.cpu().numpy()
+                    finally:
+                        eng.set_variant(-1)
+                        eng.set_shape(-1)
+                        eng.set_max_blocks(0)
+                    assert np.array_equal(st, ref_v), (variant, L, stride, shape, blocks)
+                    assert np.array_equal(got, ref_e), (variant, L, stride, shape, blocks)
+                    assert np.array_equal(est.cpu().numpy(), ref_es)
