@@ -158,8 +158,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     // 3-4 = tile kernel (csum_tile.hip: nt / plain loads), emit and verify only.
     int variant = ctx->variant;
     if (variant < 0) variant = 1;  // walk kernel, cached loads + prefetch (measured best, C2-C4)
-    if (mode == MODE_DATA && variant > 2) variant = 0;
-    const bool use_tile = variant >= 3;
+    if (mode == MODE_DATA && (variant == 3 || variant == 4)) variant = 0;
+    const bool use_tile = variant == 3 || variant == 4;
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
         hipError_t e = launch_csum(MODE_COPY, shape, 1, p, ctx->max_blocks, s);

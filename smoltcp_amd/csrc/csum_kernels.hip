@@ -286,7 +286,7 @@ __device__ __forceinline__ void line_writes(const KParams& p, const Walk& w, int
 
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
-template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF>
+template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib, u32x4* tailw, uint32_t* linfo) {
@@ -301,7 +301,9 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     const RecRef rec2 = last ? w.nxt : w.cur;
     const uint32_t nch2 = last ? n_chunks(w.nxt) : w.nch;
     const uint32_t step2 = last ? 0u : w.step + 1;
-    if (PF) load_step<G, U, NT, COPY>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
+    // SKIPD: no prefetch when the group has nothing left (one record per group in a natural grid:
+    // every record's last step would otherwise issue U loads of the dummy line)
+    if (PF && (!SKIPD || have2)) load_step<G, U, NT, COPY>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
@@ -591,6 +593,9 @@ template <int G, int U, int MODE, bool IMPLICIT, int VAR>
 __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool NT = VAR != 1;
     constexpr bool PF = VAR != 2;
+    // no prefetch once the group has nothing left: measured 1-1.5 % faster (C2 verify 0.2444 ->
+    // 0.2422 ms, C4 0.2219 -> 0.2189 ms) than loading the dummy line
+    constexpr bool SKIPD = true;
     constexpr bool COPY = MODE == MODE_COPY;
     constexpr int GPB = 256 / G;
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
@@ -623,13 +628,13 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
         load_step<G, U, NT, COPY>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
         }
     } else {
         while (true) {
             load_step<G, U, NT, COPY>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy);
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF>(p, w, va, va, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD>(p, w, va, va, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
         }
     }
 }
