@@ -35,27 +35,27 @@ int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum
 
 /* Force a launch shape for the next batched calls on this context (-1 = automatic).  A shape is
  * (lanes per record) x (16-byte chunks per lane per step):
- * 0: 8 x 6, 1: 16 x 3, 2: 16 x 6, 3: 32 x 3, 4: 32 x 4, 5: 64 x 2, 6: 64 x 4. */
+ * 0: 8 x 6, 1: 16 x 3, 2: 16 x 6, 3: 32 x 3, 4: 32 x 4, 5: 64 x 2, 6: 64 x 4, 7: 8 x 7, 8: 16 x 4. */
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
-/* Kernel variant (-1 = automatic per mode, the default): 0 = non-temporal loads + register
- * prefetch of the next step,
- * 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch (the "walk"
- * kernel: a group parses and finishes its own record); 3 / 4 = the "tile" kernel (groups only
- * stream and sum, lanes finish 64 records at once) with non-temporal / plain loads — emit and
- * verify only (data() always uses the walk kernel). */
+/* Kernel variant (-1 = automatic: 1 for emit, 5 for verify and data()).  The
+ * "walk" kernel (a group parses and finishes its own record) reads 16-byte chunks on a grid that
+ * starts at the record's 16-byte boundary: 0 = non-temporal loads + register prefetch of the next
+ * step, 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch; or at its
+ * 128-byte line boundary: 5 = non-temporal loads + prefetch, 6 = plain loads + prefetch.
+ * 3 / 4 = the "tile" kernel (groups only stream and sum, lanes finish 64 records at once) with
+ * non-temporal / plain loads — emit and verify only (data() uses the walk kernel). */
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
 
 /* Tile kernel: records per wavefront tile, 32 (default) or 64. */
 int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records);
 
-/* Emit as read pass + scatter pass, or (default) with the field stores inside the read pass. */
-int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int on);
-
-/* Fixed-stride emit writes each checksum field as the whole 64-B line(s) holding it, rebuilt from
- * the record bytes just read (default on), instead of two 2-byte stores; a partial-line store makes
- * HBM read the line back.  Off: always the 2-byte stores (A/B measurement). */
-int smol_csum_tool_set_line_writes(smol_csum_ctx_t* ctx, int on);
+/* Emit strategy: 1 = two passes (the read pass records each record's field writes — for
+ * fixed-stride batches on the line grid also the whole 64-B line(s) holding the fields — and a
+ * scatter pass writes them afterwards: whole lines need no HBM read-modify-write), 0 = 2-byte
+ * field stores inside the read pass, -1 = automatic (the default: in-pass stores, measured
+ * faster). */
+int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int mode);
 
 /* Cap the number of workgroups per launch (0 = automatic: CUs x 8). */
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
@@ -65,7 +65,7 @@ int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
 int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint64_t bytes,
                                uint32_t* d_sink, void* stream);
 
-/* The launch shape the library picks for an implicit batch of `len`-byte records. */
+/* The launch shape the library picks for a verify over an implicit batch of `len`-byte records. */
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc);
 
 #ifdef __cplusplus

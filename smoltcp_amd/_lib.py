@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsmolcsum.so")
+# SMOLCSUM_LIB: an alternative build of the same library (A/B experiments only)
+LIB_PATH = os.environ.get("SMOLCSUM_LIB") or os.path.join(_HERE, "libsmolcsum.so")
 
 SMOL_OK, SMOL_EINVAL, SMOL_ENODEV, SMOL_EHIP, SMOL_ERANGE, SMOL_ENOMEM = 0, -1, -2, -3, -4, -5
 ERROR_NAMES = {
@@ -30,7 +31,7 @@ ABI_SYMBOLS = [
 ]
 TOOL_SYMBOLS = [
     "smol_csum_tool_synth", "smol_csum_tool_corrupt", "smol_csum_tool_set_shape",
-    "smol_csum_tool_set_variant", "smol_csum_tool_set_deferred_emit", "smol_csum_tool_set_line_writes",
+    "smol_csum_tool_set_variant", "smol_csum_tool_set_deferred_emit",
     "smol_csum_tool_set_tile",
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
 ]
@@ -102,8 +103,6 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_ctx_reserve.restype = i32
     L.smol_csum_tool_set_deferred_emit.argtypes = [vp, i32]
     L.smol_csum_tool_set_deferred_emit.restype = i32
-    L.smol_csum_tool_set_line_writes.argtypes = [vp, i32]
-    L.smol_csum_tool_set_line_writes.restype = i32
     L.smol_csum_batch_data.argtypes = [vp, vp, ctypes.POINTER(BatchC), vp, vp]
     L.smol_csum_batch_data.restype = i32
     L.smol_csum_batch_emit.argtypes = [vp, vp, ctypes.POINTER(BatchC), ctypes.POINTER(Caps), vp, vp]

@@ -20,14 +20,14 @@ struct smol_csum_ctx {
     int num_cu;
     uint32_t max_blocks;  // grid cap (kNaturalGrid: one work item per group)
     int shape;            // -1 automatic, else CFG_*
-    int variant;          // kernel variant: 0 nt + prefetch (default), 1 plain + prefetch, 2 nt only
+    int variant;          // kernel variant (-1 automatic; csum_kernels.hip VarT, 3/4 tile kernel)
     uint8_t* dummy;       // 256 zero bytes on the device (target of loads with nothing to read)
-    bool defer_emit;      // emit = read pass into a patch array + scatter pass (default off)
-    uint64_t* patch;      // emit workspace: one u64 per record of a chunk
+    int defer_emit;       // -1 automatic, 0 field stores in the read pass, 1 two-pass emit
+    uint64_t* patch;      // two-pass emit workspace: one meta word per record of a chunk
+    uint8_t* lines;       // two-pass emit workspace: one 128-B line slot per record of a chunk
     uint64_t patch_cap;   // records the workspace holds
     int tile_records;     // tile kernel: records per wavefront tile (32 or 64)
     bool max_blocks_set;  // grid cap given explicitly (tooling)
-    bool line_writes;     // fixed-stride emit writes whole 64-B lines (default on; tooling can disable)
 };
 
 namespace smolcsum {
@@ -85,10 +85,21 @@ bool caps_valid(const smol_checksum_caps_t* c) {
 // 0.244 ms vs 0.27 ms at 8 blocks per CU).
 constexpr uint32_t kNaturalGrid = 0x7fffffffu;
 
-int auto_shape(uint32_t len, bool has_desc) {
+// Kernel variant when none is forced (tools/sweep.py on MI355X, C2 / C3 / C4): verify and data()
+// read on the 128-byte line grid with non-temporal loads (C2 verify 0.2415 -> 0.2327 ms, C4
+// 0.2158 -> 0.2083 ms, C3 0.826 -> 0.815 ms); emit on the 16-byte grid with cached loads (its
+// field writes interleave with the reads: nt line-grid emit is 5 % slower, C2 0.3155 -> 0.332 ms).
+int auto_variant(int mode) { return mode == MODE_EMIT ? 1 : 5; }
+
+bool line_grid(int variant) { return variant == 5 || variant == 6; }
+
+int auto_shape(uint32_t len, bool has_desc, bool line = false) {
     if (has_desc) return CFG_G16U3;
-    const uint64_t need = (uint64_t)len + 15;  // bytes of aligned chunks a record can touch
+    const uint64_t need = (uint64_t)len + (line ? 127 : 15);  // bytes of aligned chunks a record can touch
+    // eight records per wavefront in two steps, with as few idle lanes as possible (C4's 1320-B
+    // records on the line grid: 8 x 6 0.2083 ms, 8 x 7 0.2188 ms; C2's 1500 B: 8 x 7 0.2327 ms)
     if (need <= 16 * 8 * 6 * 2) return CFG_G8U6;
+    if (line && need <= 16 * 8 * 7 * 2) return CFG_G8U7;
     if (need <= 16 * 16 * 6) return CFG_G16U6;
     if (need <= 16 * 32 * 4) return CFG_G32U4;
     return CFG_G64U4;
@@ -106,18 +117,24 @@ int check_batch(const smol_csum_batch_t* b, const void* d_buf) {
     return SMOL_OK;
 }
 
-// Emit workspace: records per deferred-emit chunk (8 B each: 64 MiB at the cap).
-constexpr uint64_t SMOL_EMIT_CHUNK = 1ull << 23;
+// Two-pass emit workspace: records per chunk (8-B meta word + 128-B line slot each: 136 MiB).
+constexpr uint64_t SMOL_EMIT_CHUNK = 1ull << 20;
+constexpr uint64_t kLineSlot = 128;
 
 int reserve_patch(smol_csum_ctx_t* ctx, uint64_t n) {
     if (n <= ctx->patch_cap) return SMOL_OK;
     DeviceGuard guard(ctx->device);
     if (ctx->patch) (void)hipFree(ctx->patch);
+    if (ctx->lines) (void)hipFree(ctx->lines);
     ctx->patch = nullptr;
+    ctx->lines = nullptr;
     ctx->patch_cap = 0;
     hipError_t e = hipMalloc(&ctx->patch, n * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&ctx->lines, n * kLineSlot);
     if (e != hipSuccess) {
+        if (ctx->patch) (void)hipFree(ctx->patch);
         ctx->patch = nullptr;
+        ctx->lines = nullptr;
         return hip_fail(e, "hipMalloc (emit workspace)");
     }
     ctx->patch_cap = n;
@@ -148,37 +165,40 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.status = d_status;
     p.dummy = ctx->dummy;
     p.num_cu = ctx->max_blocks_set ? 0u : (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);
-    p.linew = (mode == MODE_EMIT && !ctx->defer_emit && ctx->line_writes) ? 1u : 0u;
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
-    int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr);
-    // Measured on MI355X (tools/sweep.py, C2): emit runs fastest with cached loads and 8-lane
-    // groups (its in-place field writes dominate), verify / data with non-temporal loads.
-    // Variants: 0-2 = walk kernel (csum_kernels.hip: nt + prefetch / plain + prefetch / nt),
-    // 3-4 = tile kernel (csum_tile.hip: nt / plain loads), emit and verify only.
+    // Variants: 0-2, 5-6 = walk kernel (csum_kernels.hip VarT: load policy, prefetch, chunk
+    // grid), 3-4 = tile kernel (csum_tile.hip: nt / plain loads), emit and verify only.
     int variant = ctx->variant;
-    if (variant < 0) variant = 1;  // walk kernel, cached loads + prefetch (measured best, C2-C4)
+    if (variant < 0) variant = auto_variant(mode);
     if (mode == MODE_DATA && (variant == 3 || variant == 4)) variant = 0;
     const bool use_tile = variant == 3 || variant == 4;
+    int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr, line_grid(variant));
+    // Two-pass emit only on request: it trades the in-pass 2-byte stores for a meta word + line
+    // slot per record and a scatter pass, and measured slower (C2: read pass 0.301 ms + scatter
+    // 0.047 ms against 0.315 ms in one pass; the slot writes alone cost 0.049 ms).
+    const bool two_pass = ctx->defer_emit == 1;
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
         hipError_t e = launch_csum(MODE_COPY, shape, 1, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
     }
-    if (use_tile && !(mode == MODE_EMIT && ctx->defer_emit)) {
+    if (use_tile && !(mode == MODE_EMIT && two_pass)) {
         hipError_t e = launch_tile(mode, shape, variant - 3, ctx->tile_records, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         return SMOL_OK;
     }
     if (use_tile) variant = 0;
-    if (mode != MODE_EMIT || !ctx->defer_emit) {
+    if (mode != MODE_EMIT || !two_pass) {
         hipError_t e = launch_csum(mode, shape, variant, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         return SMOL_OK;
     }
-    // Deferred emit: read pass -> patch array, then the scatter pass, in chunks of at most
-    // SMOL_EMIT_CHUNK records (the workspace is reserved once per context).
+    // Two-pass emit: read pass -> meta words (+ line slots), then the scatter pass, in chunks of at
+    // most SMOL_EMIT_CHUNK records (the workspace is reserved once per context).  The first record
+    // of a chunk hands over lines only when they lie inside it (the scatter pass cannot see the
+    // previous chunk's meta words).
     const uint64_t cap = b->n < SMOL_EMIT_CHUNK ? b->n : SMOL_EMIT_CHUNK;
     int rc = reserve_patch(ctx, cap);
     if (rc != SMOL_OK) return rc;
@@ -189,6 +209,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         else q.buf = d_buf + start * b->stride;
         if (d_status) q.status = d_status + start;
         q.patch = ctx->patch;
+        q.lines = ctx->lines;
         hipError_t e = launch_csum(MODE_EMIT, shape, variant, q, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         e = launch_scatter(q, ctx->max_blocks, s);
@@ -284,10 +305,10 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
         return SMOL_ENOMEM;
     }
     c->dummy = dummy;
-    c->defer_emit = false;
+    c->defer_emit = -1;
     c->tile_records = 32;
     c->max_blocks_set = false;
-    c->line_writes = true;
+    c->lines = nullptr;
     c->patch = nullptr;
     c->patch_cap = 0;
     c->device = device;
@@ -310,6 +331,7 @@ int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
         DeviceGuard guard(ctx->device);
         (void)hipFree(ctx->dummy);
         if (ctx->patch) (void)hipFree(ctx->patch);
+        if (ctx->lines) (void)hipFree(ctx->lines);
     }
     delete ctx;
     return SMOL_OK;
@@ -390,7 +412,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 4) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 6) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }
@@ -401,15 +423,9 @@ int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records) {
     return SMOL_OK;
 }
 
-int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int on) {
-    if (!ctx) return SMOL_EINVAL;
-    ctx->defer_emit = on != 0;
-    return SMOL_OK;
-}
-
-int smol_csum_tool_set_line_writes(smol_csum_ctx_t* ctx, int on) {
-    if (!ctx) return SMOL_EINVAL;
-    ctx->line_writes = on != 0;
+int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 1) return SMOL_EINVAL;
+    ctx->defer_emit = mode;
     return SMOL_OK;
 }
 
@@ -430,6 +446,8 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
     return e == hipSuccess ? SMOL_OK : hip_fail(e, "stream-read kernel launch");
 }
 
-int smol_csum_tool_auto_shape(uint32_t len, int has_desc) { return auto_shape(len, has_desc != 0); }
+int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
+    return auto_shape(len, has_desc != 0, line_grid(auto_variant(MODE_VERIFY)));
+}
 
 }  // extern "C"

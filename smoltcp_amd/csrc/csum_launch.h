@@ -20,7 +20,9 @@ enum {
     CFG_G32U4 = 4,
     CFG_G64U2 = 5,
     CFG_G64U4 = 6,
-    CFG_COUNT = 7
+    CFG_G8U7 = 7,
+    CFG_G16U4 = 8,
+    CFG_COUNT = 9
 };
 
 struct KParams {
@@ -34,11 +36,11 @@ struct KParams {
     uint16_t* out16;  // MODE_DATA
     uint8_t* status;  // MODE_VERIFY (required), MODE_EMIT (optional)
     const uint8_t* dummy;  // 16-byte-aligned device line read by loads that have nothing to read
-    uint64_t* patch;       // MODE_EMIT: deferred field writes (one u64 per record) or nullptr
+    uint64_t* patch;       // MODE_EMIT two-pass: one meta word per record (csum_kernels.hip) or nullptr
     uint32_t num_cu;       // compute units of the device (grid sizing)
     const uint8_t* src;             // MODE_COPY: payload source buffer
     const smol_csum_copy_t* copy;   // MODE_COPY: one payload copy per record (16-B aligned)
-    uint32_t linew;                 // MODE_EMIT, fixed stride: write whole 64-B lines (see csum_kernels.hip)
+    uint8_t* lines;  // MODE_EMIT two-pass, fixed stride: 128-B line slot per record (or nullptr)
 };
 
 // A dispatch may hold at most 2^32 - 1 work-items: 256-thread grids are capped at 2^24 - 1 blocks
@@ -55,6 +57,9 @@ __host__ __device__ inline uint32_t grid_blocks(uint64_t want, uint64_t cap) {
 uint32_t resident_blocks(const void* kernel, uint32_t num_cu, uint32_t max_blocks);
 
 hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s);
+// Walk kernel for one (mode, batch form): csum_walk.h, instantiated in csum_walk_*.hip.
+template <int MODE, bool IMPLICIT>
+hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s);
 hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s);
 // Tile kernel (csum_tile.hip), emit / verify only; var 0 = non-temporal loads, 1 = plain loads.
 hipError_t launch_tile(int mode, int shape, int var, int tile_records, const KParams& p, uint32_t max_blocks,

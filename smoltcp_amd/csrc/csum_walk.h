@@ -1,29 +1,44 @@
 // Batched Internet-checksum kernels for MI355X (gfx950).
 //
 // One GROUP of G lanes (G = 8, 16, 32 or 64; a group never spans two wavefronts) owns one record
-// at a time and walks the batch with a grid stride (persistent grid).  The record's bytes are
-// read as 16-byte-ALIGNED chunks with non-temporal global_load_dwordx4 (lane-contiguous, fully
-// coalesced; the data is read exactly once, so it is not kept in the caches), U chunks per lane
-// per step, so a step moves G*U*16 bytes.  The next step — or the next record's first step — is
-// issued before the current one is summed, into a second register set: the loop body is written
-// once and instantiated twice with the two sets' roles swapped (no register copies, so the
-// compiler's counted s_waitcnt vmcnt leaves the prefetch in flight).  Every load instruction is
-// issued unconditionally (out-of-range chunks read a 16-byte dummy line) for the same reason:
-// a load inside a branch makes hipcc fall back to vmcnt(0).  Bytes of a chunk outside the summed
-// span are masked; an aligned chunk never crosses a page, so reading the few bytes around a
-// record is always safe.
+// at a time and walks the batch with a grid stride (with the default natural grid every group
+// owns exactly one record).  The record's bytes are read as ALIGNED 16-byte chunks with
+// global_load_dwordx4 (lane-contiguous, fully coalesced), U chunks per lane per step, so a step
+// moves G*U*16 bytes.  The chunk grid starts either at the record's 16-byte boundary or at its
+// 128-byte cache-line boundary (LINE variants): with non-temporal loads a record's first and last
+// lines must be requested whole, or the neighbouring group's request for the rest of the line
+// fetches it from HBM a second time (tools/probe_bw.hip `rec_walk`: 16-B grid + nt 5.8 TB/s,
+// line grid + nt 7.3 TB/s).  The next step — or the next record's first step — is issued before
+// the current one is summed, into a second register set: the loop body is written once and
+// instantiated twice with the two sets' roles swapped (no register copies, so the compiler's
+// counted s_waitcnt vmcnt leaves the prefetch in flight).  Every load instruction is issued
+// unconditionally (out-of-range chunks read a 16-byte dummy line) for the same reason: a load
+// inside a branch makes hipcc fall back to vmcnt(0).  Bytes of a chunk outside the summed span are
+// masked; an aligned chunk never crosses a page, so reading the bytes around a record is safe.
 //
 // Small groups amortise the per-record work (header parse, reductions, the finishing lane) over
-// several records per wavefront: at 1500-byte records a G=16 wave finishes four records per step.
+// several records per wavefront: at 1500-byte records a G=8 wave finishes eight records per step.
 //
-// The first 128 bytes of each record (8 chunks, already in registers) are copied to a per-group
-// LDS window, from which every lane reads the IP/L4 header fields the gates need; L4 header bytes
-// past the window (behind a long IPv6 Hop-by-Hop header) are read from global memory.  Per lane
-// the protocol kernels add aligned u16 words (v_sad_u16); DPP row reductions combine the group;
-// one lane finishes the record: fold, byte-swap for an odd record start (RFC 1071 §2(B)),
-// pseudo-header, gate, write.
+// The first WIN bytes of the chunk grid (128, or 256 on the line grid: at least the record's
+// first 128 bytes, already in registers) are copied to a per-group LDS window, from which every
+// lane reads the IP/L4 header fields the gates need; L4 header bytes past the window (behind a
+// long IPv6 Hop-by-Hop header) are read from global memory.  Per lane the protocol kernels add
+// aligned u16 words (v_sad_u16); DPP row reductions combine the group; one lane finishes the
+// record: fold, byte-swap for an odd record start (RFC 1071 §2(B)), pseudo-header, gate, write.
+//
+// Emit writes two 2-byte fields per record.  In place, each is a partial-line write that HBM
+// merges with a read-modify-write, interleaved with the read stream (tools/probe_wr.hip: ~0.1 ms
+// per 2^20 records at 1.5 KB).  The two-pass emit (p.patch != nullptr) instead records one meta
+// word per record and, for fixed-stride batches on the line grid, copies the patched 64-byte
+// line(s) holding the fields from the LDS window to a compact workspace; scatter_kernel then
+// writes whole lines (no HBM read-modify-write) after the read pass.
 //
 // See csum_device.h for the arithmetic and the reference lines each rule follows.
+//
+// This header holds the kernel templates; the csum_walk_*.hip translation units instantiate them
+// per (mode, batch form) so that the build compiles them in parallel.
+#pragma once
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,7 +47,26 @@
 
 namespace smolcsum {
 
-constexpr int WIN_BYTES = 128;
+#ifndef SMOL_SKIPD
+#define SMOL_SKIPD 1  // experiments build a copy with -DSMOL_SKIPD=0
+#endif
+
+// Kernel variants: load cache policy, register prefetch, chunk-grid alignment.
+// 0 = nt + prefetch, 1 = plain + prefetch, 2 = nt without prefetch (16-byte grid);
+// 5 = nt + prefetch, 6 = plain + prefetch (128-byte line grid).  3 / 4 are the tile kernel.
+template <int VAR>
+struct VarT {
+    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5;
+    static constexpr bool PF = VAR != 2;
+    static constexpr bool LINE = VAR == 5 || VAR == 6;
+};
+
+template <bool LINE>
+struct Grid {
+    static constexpr uint64_t ALIGN = LINE ? 128 : 16;  // chunk-grid origin: record start rounded down
+    static constexpr int WIN = LINE ? 256 : 128;        // LDS window bytes (from the grid origin)
+    static constexpr int WIN_CH = WIN / 16;
+};
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -87,9 +121,11 @@ __device__ __forceinline__ RecRef rec_at(const KParams& p, uint64_t r) {
     return rr;
 }
 
+// Aligned chunks of the record's grid (from the grid origin to the chunk holding the last byte).
+template <bool LINE>
 __device__ __forceinline__ uint32_t n_chunks(const RecRef& rr) {
     if (rr.len == 0) return 0;
-    return (uint32_t)(((rr.a0 + rr.len + 15) >> 4) - (rr.a0 >> 4));
+    return (uint32_t)(((rr.a0 + rr.len + 15) >> 4) - ((rr.a0 & ~(Grid<LINE>::ALIGN - 1)) >> 4));
 }
 
 template <bool NT>
@@ -113,10 +149,11 @@ struct Regs<U, true> {
 // not exist) read the dummy line instead.  MODE_COPY: chunks entirely inside the payload are not
 // read from the record (they are replaced), and the source chunks are read only where they hold
 // payload bytes (so no load ever leaves the source range's aligned chunks).
-template <int G, int U, bool NT, bool COPY>
+template <int G, int U, bool NT, bool COPY, bool LINE>
 __device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, uint32_t nch,
                                           uint32_t step, int lane, bool valid, uint64_t dummy) {
-    const uint64_t base = rr.a0 & ~15ull;
+    static_assert(!(COPY && LINE), "MODE_COPY uses the 16-byte grid");
+    const uint64_t base = rr.a0 & ~(Grid<LINE>::ALIGN - 1);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t k = step * (G * U) + u * G + lane;
@@ -207,12 +244,17 @@ __device__ __forceinline__ uint32_t sum_masked_words(const u32x4& c, int lo, int
     return add_words(mask_dword(c.w, lo - 12, hi - 12), acc);
 }
 
-// Emit patch word, one per record when the field writes are deferred to scatter_kernel:
-// bits 0-15 IPv4 header checksum, 16-31 L4 checksum, 32-55 L4 field offset in the record,
-// PATCH_IP / PATCH_L4 = write that field, PATCH_ETH = the IPv4 header sits behind Ethernet.
-constexpr uint64_t PATCH_IP = 1ull << 56;
-constexpr uint64_t PATCH_L4 = 1ull << 57;
-constexpr uint64_t PATCH_ETH = 1ull << 58;
+
+// Two-pass emit, meta word per record (p.patch[r]):
+//   bits  0-13 record offset of the IPv4 header-checksum field (MF_NONE: no field), bit 15 MF_LINES
+//   bits 16-29 record offset of the L4 checksum field (MF_NONE: no field)
+//   bits 32-47 / 48-63 the values to write there (host order, stored big-endian).
+// MF_LINES: the 64-B line(s) holding the fields, fields patched in, sit in the record's 128-B
+// workspace slot p.lines + 128 r.  Field offsets are < 0x3fff (at most Ethernet + IPv6 + a
+// 2048-byte Hop-by-Hop header + 16).
+constexpr uint32_t MF_NONE = 0x3fffu;
+constexpr uint32_t MF_LINES = 0x8000u;
+constexpr uint32_t LINE_SLOT = 128;  // workspace bytes per record (two 64-B lines)
 
 // Per-group walk state.
 struct Walk {
@@ -228,82 +270,45 @@ struct Walk {
 
 constexpr uint32_t NO_FIELD = 0x3fffffffu;
 
-// Emit line writes (fixed-stride emit, groups of <= 32 lanes).  A 2-byte field store is a
-// partial-line write: HBM reads the 64-B line back to merge it (tools/probe_wr.hip: full 64-B line
-// stores cost ~20 % less than two 2-B stores in the same line).  So the fields are written as the
-// whole 64-B line(s) that hold them, assembled from the LDS window (this record's first 128 B,
-// fields patched in) and, for the bytes before the record, from the previous record's last chunks,
-// which the neighbouring group of the same wavefront published in LDS at the same step.  Bytes of
-// another record are rewritten with the values just read, so a line write is used only when the
-// previous record (i) is adjacent (stride == len) and handled by this wavefront in this step,
-// (ii) has its last LW_TAIL chunks in LDS, and (iii) has no checksum field inside the line; the
-// line must also end inside this record and inside the window.  Otherwise the two 2-byte stores.
-template <int G, int MODE, bool IMPLICIT>
-struct LineWrites {
-    static constexpr bool value = MODE == MODE_EMIT && IMPLICIT && G <= 32;
+// The 64-B lines a record's emit writes: [l0, l0 + 64 * nl) covering the bytes of both fields.
+// nl == 0 when the fields need more than two consecutive lines.
+struct FieldLines {
+    uint64_t l0;
+    uint32_t nl;
 };
-constexpr uint32_t LW_TAIL = 5;  // chunks of a record's tail published for the next record
-
-template <int G>
-__device__ __forceinline__ void line_writes(const KParams& p, const Walk& w, int lane, int gib, u32x4* win,
-                                            const u32x4* tailw, const uint32_t* linfo, uint64_t patch_lane0) {
-    wave_lds_sync();
-    const uint32_t* me = linfo + gib * 4;
-    const uint64_t a0 = w.cur.a0;
-    const uint64_t base = a0 & ~15ull;
-    const uint32_t fip = me[2], fl4 = me[3];
-    const bool mine = me[0] == (uint32_t)w.r + 1u;  // this group published in this step
-    const bool any = mine && (fip != NO_FIELD || fl4 != NO_FIELD);
-    const uint64_t L1 = ((a0 + (fip != NO_FIELD ? fip : fl4)) & ~63ull);
-    const uint64_t L2 = ((a0 + (fl4 != NO_FIELD ? fl4 : fip)) & ~63ull);
-    // no 2-byte field may straddle a line boundary (odd strides): both bytes must be in the lines
-    bool ok = any && (gib % (64 / G)) != 0 && p.stride == p.len && w.r > 0 &&
-              (fip == NO_FIELD || ((a0 + fip) & 63u) != 63u) && (fl4 == NO_FIELD || ((a0 + fl4) & 63u) != 63u);
-    uint64_t tA = 0;
-    if (ok) {
-        const uint32_t* nb = linfo + (gib - 1) * 4;
-        const uint64_t a0p = a0 - p.stride;
-        const uint32_t nchp = (uint32_t)(((a0p + p.len + 15) >> 4) - (a0p >> 4));
-        tA = (a0p & ~15ull) + 16ull * (nchp - LW_TAIL);
-        ok = nb[0] == (uint32_t)(w.r - 1) + 1u && nb[1] != 0u && L1 >= tA && L2 + 64 <= a0 + p.len &&
-             L2 + 64 <= base + WIN_BYTES;
-        if (ok && nb[2] != NO_FIELD) ok = !(a0p + nb[2] + 2 > L1 && a0p + nb[2] < L2 + 64);
-        if (ok && nb[3] != NO_FIELD) ok = !(a0p + nb[3] + 2 > L1 && a0p + nb[3] < L2 + 64);
-    }
-    if (ok) {
-        const uint32_t nc = L2 == L1 ? 4u : 8u;
-        for (uint32_t c = (uint32_t)lane; c < nc; c += G) {
-            const uint64_t ca = (c < 4 ? L1 : L2) + 16ull * (c & 3u);
-            const u32x4 v = ca >= base ? win[(ca - base) >> 4] : tailw[(gib - 1) * LW_TAIL + ((ca - tA) >> 4)];
-            *(GMEM u32x4*)ca = v;
-        }
-    } else if (lane == 0 && any) {
-        const gu8 wrec = (gu8)a0;
-        if (fip != NO_FIELD) store_be16(wrec + fip, (uint32_t)(patch_lane0 & 0xffffu));
-        if (fl4 != NO_FIELD) store_be16(wrec + fl4, (uint32_t)((patch_lane0 >> 16) & 0xffffu));
-    }
+__device__ __forceinline__ FieldLines field_lines(uint64_t a0, uint32_t fip, uint32_t fl4) {
+    const bool hi4 = fip != MF_NONE, hl4 = fl4 != MF_NONE;
+    const uint64_t lo = a0 + (hi4 && hl4 ? min(fip, fl4) : hi4 ? fip : fl4);
+    const uint64_t hi = a0 + 1 + (hi4 && hl4 ? max(fip, fl4) : hi4 ? fip : fl4);
+    FieldLines f;
+    f.l0 = lo & ~63ull;
+    const uint64_t l1 = hi & ~63ull;
+    f.nl = l1 == f.l0 ? 1u : (l1 == f.l0 + 64 ? 2u : 0u);
+    return f;
 }
 
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
-template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD>
+template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
-                                          int gib, u32x4* tailw, uint32_t* linfo) {
+                                          uint32_t* gsh) {
     constexpr bool COPY = MODE == MODE_COPY;
     constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
-    constexpr bool LW = LineWrites<G, MODE, IMPLICIT>::value;
+    constexpr int WIN = Grid<LINE>::WIN;
+    constexpr int WIN_CH = Grid<LINE>::WIN_CH;
+    static_assert(G * U >= WIN_CH, "step 0 must cover the LDS window");
     const uint8_t* winb = reinterpret_cast<const uint8_t*>(win);
     const uint32_t nsteps = w.nch == 0 ? 1u : (w.nch + (G * U) - 1) / (G * U);
     const bool last = w.step + 1 >= nsteps;
     const uint64_t r2 = last ? w.r + ngroups : w.r;
     const bool have2 = r2 < p.n;
     const RecRef rec2 = last ? w.nxt : w.cur;
-    const uint32_t nch2 = last ? n_chunks(w.nxt) : w.nch;
+    const uint32_t nch2 = last ? n_chunks<LINE>(w.nxt) : w.nch;
     const uint32_t step2 = last ? 0u : w.step + 1;
     // SKIPD: no prefetch when the group has nothing left (one record per group in a natural grid:
     // every record's last step would otherwise issue U loads of the dummy line)
-    if (PF && (!SKIPD || have2)) load_step<G, U, NT, COPY>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
+    if (PF && (!SKIPD || have2)) load_step<G, U, NT, COPY, LINE>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
@@ -312,11 +317,12 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
         if (last) nxt2 = t;
     }
 
-    const uint32_t head = (uint32_t)(w.cur.a0 & 15u);
+    const uint64_t base = w.cur.a0 & ~(Grid<LINE>::ALIGN - 1);
+    const uint32_t head = (uint32_t)(w.cur.a0 - base);
     // record byte o: LDS window when inside it, else global memory (long IPv6 extension chains)
     auto rd = [&](uint32_t o) -> uint32_t {
         const uint32_t x = head + o;
-        if (x < (uint32_t)WIN_BYTES) return (uint32_t)winb[x];
+        if (x < (uint32_t)WIN) return (uint32_t)winb[x];
         if (COPY && o >= w.cur.p0 && o < w.cur.p1) return ld_byte_sync(w.cur.sb + o);
         return ld_byte_sync(w.cur.a0 + o);
     };
@@ -348,7 +354,13 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
         if (MODE == MODE_DATA) {
             w.s1 = (int)w.cur.len;
         } else {
-            if (lane < WIN_BYTES / 16 && (uint32_t)lane < w.nch) win[lane] = cm[0];
+            // the window: chunks 0 .. WIN_CH-1 of the grid (chunk k = u * G + lane at step 0)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (u * G >= WIN_CH) break;
+                const uint32_t k = (uint32_t)(u * G + lane);
+                if (k < (uint32_t)WIN_CH && k < w.nch) win[k] = cm[u];
+            }
             wave_lds_sync();
             if (COPY && (w.cur.kind & KIND_BAD_COPY)) {
                 w.g = Geom{};
@@ -365,7 +377,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
         }
     }
     if constexpr (COPY) {  // store the payload bytes of this step (all of them, summed or not)
-        const gu8 base = (gu8)(w.cur.a0 & ~15ull);
+        const gu8 cbase = (gu8)base;
         const int f0b = (int)w.fip, f1b = (int)w.fl4;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -375,7 +387,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             if (k < w.nch && w.cur.p1 > w.cur.p0 && hi > 0 && lo < 16) {
                 const int f0 = f0b - pos, f1 = f1b - pos;
                 const bool field = (f0 > -2 && f0 < 16) || (f1 > -2 && f1 < 16);
-                const gu8 dst = base + 16u * k;
+                const gu8 dst = cbase + 16u * k;
                 if (lo <= 0 && hi >= 16 && !field) {
                     *(GMEM u32x4*)dst = cm[u];
                 } else {
@@ -404,7 +416,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     for (int u = 0; u < U; ++u) {
         const uint32_t k = w.step * (G * U) + u * G + lane;
         const int pos = (int)(16u * k) - (int)head;  // chunk start relative to the record
-        if (k < w.nch && pos < s1) {
+        if (k < w.nch && pos < s1 && pos + 16 > 0) {
             const u32x4 c = cm[u];
             if (pos < 0 || pos + 16 > s1) {  // first chunk (bytes before the record) / tail
                 if (MODE == MODE_DATA) {
@@ -430,16 +442,6 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     if (last) {
         const bool odd = (w.cur.a0 & 1u) != 0;
         const uint64_t r = w.r;
-        const bool lw = LW && p.linew;
-        if constexpr (LW) {
-            if (lw) {  // the record's last LW_TAIL chunks, for the next record's line writes
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t k = w.step * (G * U) + u * G + lane;
-                    if (k < w.nch && k + LW_TAIL >= w.nch) tailw[gib * LW_TAIL + (k + LW_TAIL - w.nch)] = cm[u];
-                }
-            }
-        }
         if (MODE == MODE_DATA) {
             // exact little-endian word sum relative to the span start, modulo 2^32
             const uint32_t s_rel = odd ? (w.acc2 + (w.acc << 8)) : (w.acc + (w.acc2 << 8));
@@ -476,17 +478,17 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             pre = group_sum<G>(pre);
             hsum = group_sum<G>(hsum);
             psum = group_sum<G>(psum);
-            uint64_t patch = 0;  // emit: the field writes of this record (see PATCH_* below)
             const gu8 wrec = (gu8)w.cur.a0;
             if (lane == 0) {
                 uint32_t st = g.st;
+                uint32_t fip = MF_NONE, fl4 = MF_NONE, vip = 0, vl4 = 0;  // emit: the field writes
                 // IPv4 header: data(header) (canonical fold of the big-endian word sum)
                 uint32_t ip_valid = 1, ip_ok = 1;
                 if (g.fam == 4) {
                     const uint32_t hdr = fold32(hsum);
                     if (EMITS) {
-                        const uint32_t v = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
-                        patch |= (uint64_t)v | PATCH_IP | (g.ip_off ? PATCH_ETH : 0ull);
+                        fip = g.ip_off + 10;
+                        vip = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
                     } else {
                         ip_valid = hdr == 0xffffu;
                         ip_ok = caps_rx(p.caps_ipv4) ? ip_valid : 1u;
@@ -525,7 +527,8 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                         const bool fill = g.proto == P_IGMP ? true : caps_tx(gate_caps);
                         uint32_t c = ~comb & 0xffffu;
                         if (g.proto == P_UDP && c == 0) c = 0xffffu;  // udp.rs:207
-                        patch |= ((uint64_t)(fill ? c : 0u) << 16) | ((uint64_t)fpos << 32) | PATCH_L4;
+                        fl4 = fpos;
+                        vl4 = fill ? c : 0u;
                     } else {
                         l4_valid = comb == 0xffffu;
                         if (g.proto == P_UDP && field == 0) l4_valid = 1;  // udp.rs:138-140
@@ -535,29 +538,30 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                 }
                 if (EMITS) {
                     if (!COPY && p.patch) {
-                        // deferred: the scatter pass writes the fields after every read is done
-                        ((GMEM uint64_t*)p.patch)[r] = patch;
-                    } else if (!lw) {
-                        if (patch & PATCH_IP) store_be16(wrec + g.ip_off + 10, (uint32_t)(patch & 0xffffu));
-                        if (patch & PATCH_L4) store_be16(wrec + ((patch >> 32) & 0xffffffu), (uint32_t)((patch >> 16) & 0xffffu));
+                        // two-pass emit: the fields are written by scatter_kernel after the read
+                        // pass.  Fixed-stride batches on the line grid hand over whole 64-B lines
+                        // when they lie in the window, inside the batch buffer and end inside
+                        // this record (bytes before the record are the previous record's or the
+                        // gap's; scatter_kernel checks the previous record's fields).
+                        uint32_t lines = 0;
+                        if (IMPLICIT && LINE && p.lines && p.stride >= 256 && (fip != MF_NONE || fl4 != MF_NONE)) {
+                            const FieldLines fl = field_lines(w.cur.a0, fip, fl4);
+                            const uint64_t lend = fl.l0 + 64ull * fl.nl;
+                            if (fl.nl && fl.l0 >= (uint64_t)p.buf && lend <= w.cur.a0 + w.cur.len &&
+                                lend <= base + (uint64_t)WIN) {
+                                uint8_t* wb = reinterpret_cast<uint8_t*>(win);
+                                if (fip != MF_NONE) { wb[head + fip] = (uint8_t)(vip >> 8); wb[head + fip + 1] = (uint8_t)vip; }
+                                if (fl4 != MF_NONE) { wb[head + fl4] = (uint8_t)(vl4 >> 8); wb[head + fl4 + 1] = (uint8_t)vl4; }
+                                lines = (uint32_t)((fl.l0 - base) >> 4) | (fl.nl << 8);
+                            }
+                        }
+                        *gsh = lines;
+                        ((GMEM uint64_t*)p.patch)[r] = (uint64_t)(fip | (lines ? MF_LINES : 0u)) |
+                                                       ((uint64_t)fl4 << 16) | ((uint64_t)vip << 32) |
+                                                       ((uint64_t)vl4 << 48);
                     } else {
-                        // line writes: publish the fields and patch them into the LDS window
-                        uint8_t* wb = reinterpret_cast<uint8_t*>(win);
-                        const uint32_t fip = (patch & PATCH_IP) ? g.ip_off + 10 : NO_FIELD;
-                        const uint32_t fl4 = (patch & PATCH_L4) ? (uint32_t)((patch >> 32) & 0xffffffu) : NO_FIELD;
-                        if (fip != NO_FIELD && head + fip + 1 < (uint32_t)WIN_BYTES) {
-                            wb[head + fip] = (uint8_t)(patch >> 8);
-                            wb[head + fip + 1] = (uint8_t)patch;
-                        }
-                        if (fl4 != NO_FIELD && head + fl4 + 1 < (uint32_t)WIN_BYTES) {
-                            wb[head + fl4] = (uint8_t)(patch >> 24);
-                            wb[head + fl4 + 1] = (uint8_t)(patch >> 16);
-                        }
-                        const bool tail_ok = w.nch >= LW_TAIL && (w.nch - LW_TAIL) >= w.step * (G * U);
-                        linfo[gib * 4 + 0] = (uint32_t)r + 1u;
-                        linfo[gib * 4 + 1] = tail_ok ? 1u : 0u;
-                        linfo[gib * 4 + 2] = fip;
-                        linfo[gib * 4 + 3] = fl4;
+                        if (fip != MF_NONE) store_be16(wrec + fip, vip);
+                        if (fl4 != MF_NONE) store_be16(wrec + fl4, vl4);
                     }
                     if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
                 } else {
@@ -569,8 +573,20 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                     ((gu8)p.status)[r] = (uint8_t)st;
                 }
             }
-            if constexpr (LW) {
-                if (lw) line_writes<G>(p, w, lane, gib, win, tailw, linfo, patch);
+            if constexpr (MODE == MODE_EMIT && IMPLICIT && LINE) {
+                if (p.patch && p.lines) {  // copy the patched line(s) from the window to the slot
+                    wave_lds_sync();
+                    const uint32_t lines = *gsh;
+#if defined(SMOL_EXP_NOSLOT)
+                    const uint32_t nc = 0, c0 = lines & 0xffu;  // experiment: no slot copies
+#elif defined(SMOL_EXP_SLOT64)
+                    const uint32_t nc = lines ? 4u : 0u, c0 = lines & 0xffu;  // experiment: one line only
+#else
+                    const uint32_t nc = 4u * (lines >> 8), c0 = lines & 0xffu;
+#endif
+                    for (uint32_t c = (uint32_t)lane; c < nc; c += G)
+                        *(GMEM u32x4*)((uint64_t)p.lines + (uint64_t)LINE_SLOT * r + 16u * c) = win[c0 + c];
+                }
             }
         }
     }
@@ -586,23 +602,22 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 }
 
 // MODE_DATA: checksum::data over [0, len).  MODE_EMIT / MODE_VERIFY: the protocol gates.
-// MODE_COPY: payload copy + emit in one pass.
-// VAR: 0 = non-temporal loads + register prefetch, 1 = plain loads + prefetch (default),
-// 2 = non-temporal loads, no prefetch (each step loads then waits; occupancy hides latency).
+// MODE_COPY: payload copy + emit in one pass.  VAR: see VarT.
 template <int G, int U, int MODE, bool IMPLICIT, int VAR>
 __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
-    constexpr bool NT = VAR != 1;
-    constexpr bool PF = VAR != 2;
-    // no prefetch once the group has nothing left: measured 1-1.5 % faster (C2 verify 0.2444 ->
-    // 0.2422 ms, C4 0.2219 -> 0.2189 ms) than loading the dummy line
-    constexpr bool SKIPD = true;
+    constexpr bool NT = VarT<VAR>::NT;
+    constexpr bool PF = VarT<VAR>::PF;
+    constexpr bool LINE = VarT<VAR>::LINE;
+    // Fixed-stride batches: no prefetch once the group has nothing left (one record per group in
+    // a natural grid), measured 1-1.5 % faster (C2 verify 0.2444 -> 0.2422 ms, C4 0.2219 -> 0.2189
+    // ms).  Descriptor batches keep the unconditional prefetch: there the conditional load made
+    // C3 verify 25 % slower (0.810 -> 0.989 ms).
+    constexpr bool SKIPD = SMOL_SKIPD && IMPLICIT;
     constexpr bool COPY = MODE == MODE_COPY;
     constexpr int GPB = 256 / G;
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
-    __shared__ u32x4 win[GPB][WIN_BYTES / 16];
-    constexpr bool LW = LineWrites<G, MODE, IMPLICIT>::value;
-    __shared__ u32x4 tailw[LW ? GPB * LW_TAIL : 1];
-    __shared__ uint32_t linfo[LW ? GPB * 4 : 1];
+    __shared__ u32x4 win[GPB][Grid<LINE>::WIN_CH];
+    __shared__ uint32_t gsh[GPB];
 
     const int lane = (int)(threadIdx.x % G);
     const int gib = (int)(threadIdx.x / G);
@@ -612,43 +627,46 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     if (w.r >= p.n) return;
     w.cur = rec_at<IMPLICIT, COPY>(p, w.r);
     w.nxt = rec_at<IMPLICIT, COPY>(p, w.r + ngroups < p.n ? w.r + ngroups : p.n - 1);
-    w.nch = n_chunks(w.cur);
+    w.nch = n_chunks<LINE>(w.cur);
     w.step = 0;
     w.g = Geom{};
     w.s1 = 0;
     w.acc = w.acc2 = 0;
     w.fip = w.fl4 = NO_FIELD;
-    if (LW) {
-        for (int i = lane; i < 4; i += G) linfo[gib * 4 + i] = 0u;
-    }
 
     Regs<U, COPY> va;
     if (PF) {
         Regs<U, COPY> vb;
-        load_step<G, U, NT, COPY>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
+        load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, va, vb, lane, ngroups, &win[gib][0], &gsh[gib])) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, vb, va, lane, ngroups, &win[gib][0], &gsh[gib])) break;
         }
     } else {
         while (true) {
-            load_step<G, U, NT, COPY>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy);
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD>(p, w, va, va, lane, ngroups, &win[gib][0], gib, tailw, linfo)) break;
+            load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy);
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, va, va, lane, ngroups, &win[gib][0], &gsh[gib])) break;
         }
     }
 }
 
-// Second pass of a deferred emit: one lane per record applies the patch word.  Writing the 2-byte
-// fields inside the read pass interleaves a scattered write with every 1.5 KB of streamed reads,
-// which cost ~40 % of a read pass on MI355X (tools/probe_wr.hip); a compact patch array (+5 %)
-// plus this write-only pass is far cheaper.
+// Second pass of the two-pass emit: 8 lanes per record apply its meta word.  MF_LINES records
+// write their whole 64-B line(s) from the workspace slot — unless a field of the previous record
+// lies inside them (its bytes in the slot are the pre-emit ones), then, like every other record,
+// they store the two 2-byte fields.  A record's lines end inside the record and start at most
+// 63 bytes before it, and records are >= 256 bytes apart, so only the previous record can meet
+// them, and only it can have a field there.
 template <bool IMPLICIT>
 __global__ __launch_bounds__(256) void scatter_kernel(KParams p) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += stride) {
-        const uint64_t patch = ((const GMEM uint64_t*)p.patch)[r];
-        if (!(patch & (PATCH_IP | PATCH_L4))) continue;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < 8 * p.n; t += stride) {
+        const uint64_t r = t >> 3;
+        const uint32_t c = (uint32_t)(t & 7u);
+        const uint64_t m = ((const GMEM uint64_t*)p.patch)[r];
+        const uint32_t fip = (uint32_t)m & MF_NONE, fl4 = (uint32_t)(m >> 16) & MF_NONE;
+        const uint32_t vip = (uint32_t)(m >> 32) & 0xffffu, vl4 = (uint32_t)(m >> 48);
+        if (fip == MF_NONE && fl4 == MF_NONE) continue;
         uint64_t a0;
         if (IMPLICIT) {
             a0 = (uint64_t)p.buf + r * p.stride;
@@ -656,17 +674,27 @@ __global__ __launch_bounds__(256) void scatter_kernel(KParams p) {
             const GMEM uint64_t* d = (const GMEM uint64_t*)((uint64_t)p.desc + 16 * r);
             a0 = (uint64_t)p.buf + d[0];
         }
-        if (patch & PATCH_IP) store_be16((gu8)(a0 + ((patch & PATCH_ETH) ? 24 : 10)), (uint32_t)(patch & 0xffffu));
-        if (patch & PATCH_L4) store_be16((gu8)(a0 + ((patch >> 32) & 0xffffffu)), (uint32_t)((patch >> 16) & 0xffffu));
+        bool as_lines = IMPLICIT && (m & MF_LINES);
+        FieldLines fl = {0, 0};
+        if (as_lines) {
+            fl = field_lines(a0, fip, fl4);
+            if (r > 0) {
+                const uint64_t mp = ((const GMEM uint64_t*)p.patch)[r - 1];
+                const uint64_t ap = a0 - p.stride;
+                const uint64_t lend = fl.l0 + 64ull * fl.nl;
+                const uint32_t pf[2] = {(uint32_t)mp & MF_NONE, (uint32_t)(mp >> 16) & MF_NONE};
+                for (int i = 0; i < 2; ++i)
+                    if (pf[i] != MF_NONE && ap + pf[i] + 2 > fl.l0 && ap + pf[i] < lend) as_lines = false;
+            }
+        }
+        if (as_lines) {
+            if (c < 4 * fl.nl)
+                *(GMEM u32x4*)(fl.l0 + 16u * c) = *(const GMEM u32x4*)((uint64_t)p.lines + (uint64_t)LINE_SLOT * r + 16u * c);
+        } else if (c == 0) {
+            if (fip != MF_NONE) store_be16((gu8)(a0 + fip), vip);
+            if (fl4 != MF_NONE) store_be16((gu8)(a0 + fl4), vl4);
+        }
     }
-}
-
-hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    const uint64_t want = (p.n + 255) / 256;
-    const uint32_t blocks = grid_blocks(want, max_blocks);
-    if (p.desc) hipLaunchKernelGGL(scatter_kernel<false>, dim3(blocks), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(scatter_kernel<true>, dim3(blocks), dim3(256), 0, s, p);
-    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -674,7 +702,7 @@ hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s) 
 // ---------------------------------------------------------------------------------------------
 
 template <int G, int U, int MODE, bool IMPLICIT, int VAR>
-static hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
+hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
@@ -683,10 +711,12 @@ static hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t 
 }
 
 template <int MODE, bool IMPLICIT, int VAR>
-static hipError_t launch_shape(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+hipError_t launch_shape(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (shape) {
         case CFG_G8U6: return launch_one<8, 6, MODE, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G8U7: return launch_one<8, 7, MODE, IMPLICIT, VAR>(p, max_blocks, s);
         case CFG_G16U3: return launch_one<16, 3, MODE, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G16U4: return launch_one<16, 4, MODE, IMPLICIT, VAR>(p, max_blocks, s);
         case CFG_G16U6: return launch_one<16, 6, MODE, IMPLICIT, VAR>(p, max_blocks, s);
         case CFG_G32U3: return launch_one<32, 3, MODE, IMPLICIT, VAR>(p, max_blocks, s);
         case CFG_G32U4: return launch_one<32, 4, MODE, IMPLICIT, VAR>(p, max_blocks, s);
@@ -695,44 +725,30 @@ static hipError_t launch_shape(int shape, const KParams& p, uint32_t max_blocks,
     }
 }
 
-template <int MODE>
-static hipError_t launch_mode(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    const bool implicit = p.desc == nullptr;
+template <int MODE, bool IMPLICIT>
+hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (var) {
-        case 1:
-            return implicit ? launch_shape<MODE, true, 1>(shape, p, max_blocks, s)
-                            : launch_shape<MODE, false, 1>(shape, p, max_blocks, s);
-        case 2:
-            return implicit ? launch_shape<MODE, true, 2>(shape, p, max_blocks, s)
-                            : launch_shape<MODE, false, 2>(shape, p, max_blocks, s);
-        default:
-            return implicit ? launch_shape<MODE, true, 0>(shape, p, max_blocks, s)
-                            : launch_shape<MODE, false, 0>(shape, p, max_blocks, s);
+        case 1: return launch_shape<MODE, IMPLICIT, 1>(shape, p, max_blocks, s);
+        case 2: return launch_shape<MODE, IMPLICIT, 2>(shape, p, max_blocks, s);
+        case 5: return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
+        case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
+        default: return launch_shape<MODE, IMPLICIT, 0>(shape, p, max_blocks, s);
     }
 }
 
 // MODE_COPY keeps three chunks per lane and step (record + two source chunks), so it is built for
 // the U <= 3 shapes only (wider shapes map to the same group size with fewer chunks) and for the
-// plain-load variant (measured best for emit).
+// plain-load variant on the 16-byte grid (measured best for emit).
 template <bool IMPLICIT>
-static hipError_t launch_copy(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+hipError_t launch_copy(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (shape) {
-        case CFG_G8U6: return launch_one<8, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
+        case CFG_G8U6:
+        case CFG_G8U7: return launch_one<8, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
         case CFG_G32U3:
         case CFG_G32U4: return launch_one<32, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
         case CFG_G64U2:
         case CFG_G64U4: return launch_one<64, 2, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
         default: return launch_one<16, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
-    }
-}
-
-hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    switch (mode) {
-        case MODE_DATA: return launch_mode<MODE_DATA>(shape, var, p, max_blocks, s);
-        case MODE_EMIT: return launch_mode<MODE_EMIT>(shape, var, p, max_blocks, s);
-        case MODE_COPY:
-            return p.desc == nullptr ? launch_copy<true>(shape, p, max_blocks, s) : launch_copy<false>(shape, p, max_blocks, s);
-        default: return launch_mode<MODE_VERIFY>(shape, var, p, max_blocks, s);
     }
 }
 

@@ -1,0 +1,6 @@
+// Instantiates the walk kernel (csum_walk.h) for MODE_VERIFY, descriptor batches.
+#include "csum_walk.h"
+
+namespace smolcsum {
+template hipError_t launch_walk<MODE_VERIFY, false>(int, int, const KParams&, uint32_t, hipStream_t);
+}  // namespace smolcsum

@@ -120,8 +120,8 @@ def test_auto_shape():
     from smoltcp_amd.engine import auto_shape
 
     assert auto_shape(64) == 0      # 8 lanes x 6 chunks
-    assert auto_shape(1500) == 0    # 8 x 6: eight 1500-byte records per wavefront, two steps each
-    assert auto_shape(2000) == 4    # 32 x 4
+    assert auto_shape(1500) == 7    # 8 x 7: eight 1500-byte records per wavefront, two steps each
+    assert auto_shape(1900) == 4    # 32 x 4 (line grid: up to 2048 - 127 bytes)
     assert auto_shape(9000) == 6    # 64 x 4
     assert auto_shape(1500, True) == 1  # descriptors: 16 x 3
 

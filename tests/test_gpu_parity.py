@@ -25,7 +25,7 @@ from smoltcp_amd import engine as E  # noqa: E402
 
 CAPS_DEFAULT = (0, 0, 0, 0, 0)
 V4A, V4B = bytes([192, 168, 1, 1]), bytes([192, 168, 1, 2])
-SHAPES = [0, 1, 2, 3, 4, 5, 6]
+SHAPES = [0, 1, 2, 3, 4, 5, 6, 7, 8]
 
 
 @pytest.fixture(scope="module")
@@ -444,42 +444,102 @@ def test_grid_cap_huge_batch(eng):
     assert int((st == int(ref)).sum()) == n and (ref & E.ST_ACCEPT)
 
 
+def _emit_case(eng, host, off, n, stride, L, kind, caps, variant, defer, shape=-1, blocks=0):
+    """Emit a fixed-stride batch that starts `off` bytes into `host` (a device copy of it) and
+    compare the WHOLE buffer with the oracle: bytes outside the records (before the batch, gaps,
+    neighbours rewritten by whole-line writes) must not change."""
+    full = torch.from_numpy(host.copy()).cuda()
+    d = full[off:]
+    batch = E.Batch.fixed(n, stride, L, kind)
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    eng.set_variant(variant)
+    eng.set_deferred_emit(defer)
+    eng.set_shape(shape)
+    eng.set_max_blocks(blocks)
+    try:
+        eng.emit(d, batch, caps=caps, status=st)
+        got = full.cpu().numpy()
+    finally:
+        eng.set_variant(-1)
+        eng.set_deferred_emit(None)
+        eng.set_shape(-1)
+        eng.set_max_blocks(0)
+    ref = host.copy()
+    sub = ref[off:].copy()
+    ref_st = oracle.batch_emit(sub, None, n, stride, L, kind, caps)
+    ref[off:] = sub
+    diff = np.nonzero(got != ref)[0]
+    assert diff.size == 0, (stride, L, off, variant, defer, shape, blocks, caps, diff[:8])
+    assert np.array_equal(st.cpu().numpy(), ref_st), (stride, L, off, variant, defer)
+
+
 @pytest.mark.parametrize("profile,kind", [(E.SYNTH_UDP4, E.KIND_IP), (E.SYNTH_TCP4, E.KIND_IP),
                                           (E.SYNTH_V6MIX, E.KIND_IP), (E.SYNTH_ETH_TCP4, E.KIND_ETH)])
-def test_emit_line_writes_match_oracle(eng, profile, kind):
-    """Fixed-stride emit with whole-line field writes (default) against the oracle over the whole
-    buffer (bytes of neighbouring records are rewritten by line writes and must not change):
-    strides short enough that neighbouring fields share lines, odd strides, every shape, a
-    persistent grid (several records per group), caps that write zero fields."""
-    for stride in (64, 66, 80, 97, 128, 200, 1500, 1501, 1519):
+def test_emit_two_pass_match_oracle(eng, profile, kind):
+    """Fixed-stride emit in every strategy (two-pass with whole-line writes — the default on the
+    line grid — two-pass with 2-byte stores only, stores in the read pass) against the oracle over
+    the whole buffer: strides below / at / above the 256-byte line-write threshold, odd strides and
+    odd batch starts, gaps (stride > len), every shape, persistent grids, caps that write zeros."""
+    rng = np.random.default_rng(profile)
+    for stride, L in [(64, 64), (97, 97), (200, 200), (255, 255), (256, 256), (257, 257), (300, 256),
+                      (1500, 1500), (1501, 1501), (1519, 1500), (4000, 4000)]:
         n = 1031
-        buf = torch.zeros(n * stride + 64, dtype=torch.uint8, device="cuda:0")
-        batch = E.Batch.fixed(n, stride, stride, kind)
-        eng.synth(buf, batch, profile, seed=stride * 13 + profile)
-        host = buf.cpu().numpy().copy()
-        for shape, blocks, caps in [(-1, 0, (0, 0, 0, 0, 0)), (0, 3, (0, 0, 0, 0, 0)), (1, 0, (2, 3, 0, 1, 0)),
-                                    (3, 0, (0, 0, 0, 0, 0)), (4, 5, (3, 2, 2, 3, 3))]:
-            for lw in (True, False):
-                eng.set_shape(shape)
-                eng.set_max_blocks(blocks)
-                eng.set_line_writes(lw)
-                try:
-                    d = torch.from_numpy(host.copy()).cuda()
-                    st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
-                    eng.emit(d, batch, caps=caps, status=st)
-                    got = d.cpu().numpy()
-                finally:
-                    eng.set_shape(-1)
-                    eng.set_max_blocks(0)
-                    eng.set_line_writes(True)
-                ref = host.copy()
-                ref_st = oracle.batch_emit(ref, None, n, stride, stride, kind, caps)
-                diff = np.nonzero(got != ref)[0]
-                assert diff.size == 0, (profile, stride, shape, blocks, caps, lw, diff[:8])
-                assert np.array_equal(st.cpu().numpy(), ref_st)
+        for off in (0, 37):
+            host = rng.integers(0, 256, off + n * stride + 128, dtype=np.uint8)
+            tmp = torch.from_numpy(host[off:].copy()).cuda()
+            eng.synth(tmp, E.Batch.fixed(n, stride, L, kind), profile, seed=stride * 13 + profile + off)
+            host[off:] = tmp.cpu().numpy()
+            for variant, defer, shape, blocks, caps in [
+                    (-1, None, -1, 0, (0, 0, 0, 0, 0)), (5, 1, 0, 3, (0, 0, 0, 0, 0)),
+                    (6, 1, 1, 0, (2, 3, 0, 1, 0)), (5, 1, 7, 0, (0, 0, 0, 0, 0)),
+                    (5, 1, 8, 5, (3, 2, 2, 3, 3)), (5, 0, 5, 0, (0, 0, 0, 0, 0)),
+                    (1, 1, 3, 0, (0, 0, 0, 0, 0)), (1, 0, 0, 0, (0, 0, 0, 0, 0))]:
+                _emit_case(eng, host, off, n, stride, L, kind, caps, variant, defer, shape, blocks)
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4])
+def test_emit_two_pass_neighbour_fields(eng):
+    """Whole-line field writes reach up to 63 bytes into the previous record.  Records whose L4
+    checksum field sits in their last 64 bytes (IPv6 Hop-by-Hop pushes it there) alternate with
+    IPv4 / IPv6 records whose field lines start before them: the scatter pass must fall back to
+    2-byte stores wherever a line would carry the previous record's stale field."""
+    rng = np.random.default_rng(77)
+    a6, b6 = bytes(range(16)), bytes(range(16, 32))
+    for stride in (256, 257, 300, 301, 320):
+        recs = []
+        for i in range(515):
+            k = i % 3
+            if k == 0:  # UDP field near the record end
+                units = (stride - 40 - 8 - 10) // 8 - 1
+                h = P.hbh(17, units, rng)
+                room = stride - 40 - len(h) - 8
+                body = P.ipv6(a6, b6, 0, h + P.udp(5, 6, P.rand_bytes(rng, int(rng.integers(0, room + 1)))))
+            elif k == 1:
+                body = P.ipv4(V4A, V4B, 17, P.udp(1, 2, P.rand_bytes(rng, int(rng.integers(0, stride - 28)))))
+            else:
+                body = P.ipv6(a6, b6, 6, P.tcp(7, 8, P.rand_bytes(rng, int(rng.integers(0, stride - 60)))))
+            recs.append(body + P.rand_bytes(rng, stride - len(body)))
+        n = len(recs)
+        for off in (0, 5, 40, 63):
+            host = np.concatenate([rng.integers(0, 256, off, dtype=np.uint8),
+                                   np.frombuffer(b"".join(recs), np.uint8), np.zeros(128, np.uint8)])
+            for variant, defer in [(-1, None), (5, 1), (6, 1), (1, 1)]:
+                _emit_case(eng, host, off, n, stride, stride, E.KIND_IP, CAPS_DEFAULT, variant, defer)
+
+
+def test_emit_two_pass_chunks(eng):
+    """More records than one two-pass workspace chunk (2^20): chunk boundaries, and the first
+    record of each chunk (it cannot see the previous chunk's meta words)."""
+    n, L = (1 << 20) + 37, 256
+    for stride, off in ((256, 0), (257, 11)):
+        host = np.zeros(off + n * stride + 128, dtype=np.uint8)
+        tmp = torch.zeros(n * stride + 128, dtype=torch.uint8, device="cuda:0")
+        eng.synth(tmp, E.Batch.fixed(n, stride, L, E.KIND_IP), E.SYNTH_UDP4, seed=stride)
+        host[off:] = tmp.cpu().numpy()
+        del tmp
+        _emit_case(eng, host, off, n, stride, L, E.KIND_IP, CAPS_DEFAULT, -1, None)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_variants_fixed_stride(eng, variant):
     """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
     the oracle on fixed-stride batches: strides equal to the record length (neighbours share

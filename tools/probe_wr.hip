@@ -25,6 +25,29 @@ __global__ void scatter_wt(uint8_t* buf, uint64_t n, const uint32_t* vals) {
     }
 }
 
+// full-line scatter pass: 4 lanes per record copy the record's saved 64-B field line back
+__global__ void scatter64(uint8_t* buf, uint64_t n, const uint8_t* lines) {
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < 4 * n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = t >> 2, c = t & 3;
+        const u32x4 v = *(const GMEM u32x4*)((uint64_t)lines + 16 * t);
+        *(GMEM u32x4*)((uint64_t)buf + r * 1536 + 16 * c) = v;
+    }
+}
+
+// re-read scatter: 4 lanes per record read the field line back from the record itself, patch the
+// two fields from a 4-B compact array and write the whole line (no 64-B line copy in pass 1)
+__global__ void scatter_rr(uint8_t* buf, uint64_t n, const uint32_t* vals) {
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < 4 * n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = t >> 2, c = t & 3;
+        const uint32_t v = vals[r];
+        GMEM u32x4* q = (GMEM u32x4*)((uint64_t)buf + r * 1536 + 16 * c);
+        u32x4 x = *q;
+        if (c == 0) x.z = (x.z & 0xffff0000u) | (v & 0xffffu);
+        if (c == 1) x.z = (x.z & 0xffff0000u) | (v >> 16);
+        *q = x;
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void rw(uint8_t* buf, uint64_t n, uint8_t* status) {
     const int lane = threadIdx.x & 15;
@@ -58,6 +81,10 @@ __global__ __launch_bounds__(256) void rw(uint8_t* buf, uint64_t n, uint8_t* sta
         if (MODE == 15 && lane == 0 && (r & 3) == 0) { *(GMEM uint16_t*)(a0 + 10) = (uint16_t)acc; *(GMEM uint16_t*)(a0 + 26) = (uint16_t)(acc >> 16); }
         // 64-B line store at every 2nd record
         if (MODE == 16 && lane < 4 && (r & 1) == 0) { u32x4 c = v[0]; c.x = acc; *(GMEM u32x4*)(a0 + 16 * lane) = c; }
+        // compact 64-B line array (the record's field line, patched), for a later full-line scatter
+        if (MODE == 17 && lane < 4) { u32x4 c = v[0]; c.x = acc; *(GMEM u32x4*)((uint64_t)status + 64 * r + 16 * lane) = c; }
+        // 64-B line store, non-temporal
+        if (MODE == 18 && lane < 4) { u32x4 c = v[0]; c.x = acc; __builtin_nontemporal_store(c, (GMEM u32x4*)(a0 + 16 * lane)); }
         if (MODE == 0 && acc == 0x12345678u) status[0] = 1;
     }
 }
@@ -66,15 +93,15 @@ int main() {
     const uint64_t n = 1 << 20;
     uint8_t *buf, *st;
     CK(hipMalloc(&buf, n * 1536));
-    CK(hipMalloc(&st, 4 * n));
+    CK(hipMalloc(&st, 64 * n));
     CK(hipMemset(buf, 0x33, n * 1536));
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     const char* names[] = {"read only", "2 x 2-B stores", "32-B store", "64-B line store", "128-B store", "1-B status array", "16-B store", "2 x 2-B nt stores", "4-B compact array", "scatter kernel only",
                            "2x2-B sc0 sc1", "2x2-B sc1", "2x2-B nt sc0 sc1", "2x2-B sc0", "32-B sc0 sc1",
-                           "2x2-B every 2nd", "2x2-B every 4th", "64-B every 2nd"};
+                           "2x2-B every 2nd", "2x2-B every 4th", "64-B every 2nd", "compact 64-B lines", "64-B nt line store"};
     for (int rnd = 0; rnd < 2; ++rnd)
-    for (int bpc : {2, 8}) for (int m = 0; m < 18; ++m) {
+    for (int bpc : {2, 8}) for (int m = 0; m < 20; ++m) {
         auto run = [&]() {
             switch (m) {
                 case 0: hipLaunchKernelGGL(rw<0>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
@@ -94,6 +121,8 @@ int main() {
                 case 15: hipLaunchKernelGGL(rw<14>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 case 16: hipLaunchKernelGGL(rw<15>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 case 17: hipLaunchKernelGGL(rw<16>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 18: hipLaunchKernelGGL(rw<17>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
+                case 19: hipLaunchKernelGGL(rw<18>, dim3(256 * bpc), dim3(256), 0, 0, buf, n, st); break;
                 default: hipLaunchKernelGGL(scatter, dim3(256 * bpc), dim3(256), 0, 0, buf, n, (const uint32_t*)st); break;
             }
         };
@@ -111,9 +140,11 @@ int main() {
     CK(hipMalloc(&bufB, n * 1536));
     CK(hipMemset(bufB, 0x44, n * 1536));
     const char* seqn[] = {"B read only", "A read + B read", "A 2x2B + B read", "A 64B + B read", "A compact + scatter + B read",
-                          "A compact + scatter_wt + B read", "A 2x2B sc0sc1 + B read", "A compact + scatter", "A compact + scatter_wt"};
+                          "A compact + scatter_wt + B read", "A 2x2B sc0sc1 + B read", "A compact + scatter", "A compact + scatter_wt",
+                          "A compact64 + scatter64 + B read", "A compact64 + B read", "A compact64 + scatter64", "A 64B nt + B read",
+                          "A compact + scatter_rr + B read", "A compact + scatter_rr"};
     for (int rnd = 0; rnd < 2; ++rnd)
-    for (int q = 0; q < 9; ++q) {
+    for (int q = 0; q < 15; ++q) {
         const int bpc = 2;
         auto run = [&]() {
             dim3 g(256 * bpc), b(256);
@@ -127,8 +158,14 @@ int main() {
                 case 5: case 8: hipLaunchKernelGGL(rw<8>, g, b, 0, 0, buf, n, st);
                         hipLaunchKernelGGL(scatter_wt, g, b, 0, 0, buf, n, (const uint32_t*)st); break;
                 case 6: hipLaunchKernelGGL(rw<9>, g, b, 0, 0, buf, n, st); break;
+                case 9: case 11: hipLaunchKernelGGL(rw<17>, g, b, 0, 0, buf, n, st);
+                        hipLaunchKernelGGL(scatter64, g, b, 0, 0, buf, n, st); break;
+                case 10: hipLaunchKernelGGL(rw<17>, g, b, 0, 0, buf, n, st); break;
+                case 12: hipLaunchKernelGGL(rw<18>, g, b, 0, 0, buf, n, st); break;
+                case 13: case 14: hipLaunchKernelGGL(rw<8>, g, b, 0, 0, buf, n, st);
+                        hipLaunchKernelGGL(scatter_rr, g, b, 0, 0, buf, n, (const uint32_t*)st); break;
             }
-            if (q < 7) hipLaunchKernelGGL(rw<0>, g, b, 0, 0, bufB, n, st);
+            if (q < 7 || q == 9 || q == 10 || q == 12 || q == 13) hipLaunchKernelGGL(rw<0>, g, b, 0, 0, bufB, n, st);
         };
         for (int i = 0; i < 3; ++i) run();
         CK(hipEventRecord(a, 0));

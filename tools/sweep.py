@@ -23,10 +23,10 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--shapes", default="0,1,2,3,4,5,6")
+    ap.add_argument("--shapes", default="0,1,2,3,4,5,6,7,8")
     ap.add_argument("--blocks", default="0")
     ap.add_argument("--var", default="0,1,2")
-    ap.add_argument("--defer", default="1")
+    ap.add_argument("--defer", default="-1", help="emit strategy: -1 auto, 0 in-pass stores, 1 two-pass")
     ap.add_argument("--tile", default="32")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -43,7 +43,7 @@ def main():
                                           for c in [int(x) for x in args.defer.split(",")]
                                           for d in [int(x) for x in args.tile.split(",")]]:
                 if True:
-                    eng.set_deferred_emit(bool(defer))
+                    eng.set_deferred_emit(defer)
                     eng.set_shape(shape)
                     eng.set_variant(var)
                     eng.set_tile(tile)
