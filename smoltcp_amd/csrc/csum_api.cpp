@@ -85,11 +85,12 @@ bool caps_valid(const smol_checksum_caps_t* c) {
 // 0.244 ms vs 0.27 ms at 8 blocks per CU).
 constexpr uint32_t kNaturalGrid = 0x7fffffffu;
 
-// Kernel variant when none is forced (tools/sweep.py on MI355X, C2 / C3 / C4): verify and data()
-// read on the 128-byte line grid with non-temporal loads (C2 verify 0.2415 -> 0.2327 ms, C4
-// 0.2158 -> 0.2083 ms, C3 0.826 -> 0.815 ms); emit on the 16-byte grid with cached loads (its
-// field writes interleave with the reads: nt line-grid emit is 5 % slower, C2 0.3155 -> 0.332 ms).
-int auto_variant(int mode) { return mode == MODE_EMIT ? 1 : 5; }
+// Kernel variant when none is forced (tools/sweep.py on MI355X, C2 / C3 / C4): the 128-byte line
+// grid with non-temporal loads (verify: C2 0.2415 -> 0.2327 ms, C4 0.2158 -> 0.2083 ms, C3 0.826 ->
+// 0.815 ms; fixed-stride emit with shared boundary lines, csum_walk.h shared_from: C2 0.3155 ->
+// 0.304 ms, C4 0.2727 -> 0.263 ms), except emit over descriptor batches: cached loads on the
+// 16-byte grid (C3 0.9705 ms vs 0.9722 ms).
+int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 1 : 5; }
 
 bool line_grid(int variant) { return variant == 5 || variant == 6; }
 
@@ -170,7 +171,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     // Variants: 0-2, 5-6 = walk kernel (csum_kernels.hip VarT: load policy, prefetch, chunk
     // grid), 3-4 = tile kernel (csum_tile.hip: nt / plain loads), emit and verify only.
     int variant = ctx->variant;
-    if (variant < 0) variant = auto_variant(mode);
+    if (variant < 0) variant = auto_variant(mode, b->desc != nullptr);
     if (mode == MODE_DATA && (variant == 3 || variant == 4)) variant = 0;
     const bool use_tile = variant == 3 || variant == 4;
     int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr, line_grid(variant));
@@ -447,7 +448,7 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
 }
 
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
-    return auto_shape(len, has_desc != 0, line_grid(auto_variant(MODE_VERIFY)));
+    return auto_shape(len, has_desc != 0, line_grid(auto_variant(MODE_VERIFY, has_desc != 0)));
 }
 
 }  // extern "C"

@@ -149,15 +149,18 @@ struct Regs<U, true> {
 // not exist) read the dummy line instead.  MODE_COPY: chunks entirely inside the payload are not
 // read from the record (they are replaced), and the source chunks are read only where they hold
 // payload bytes (so no load ever leaves the source range's aligned chunks).
+// Chunks at addresses >= lim are not loaded (they come from the next record's LDS window, see
+// shared_from).
 template <int G, int U, bool NT, bool COPY, bool LINE>
 __device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, uint32_t nch,
-                                          uint32_t step, int lane, bool valid, uint64_t dummy) {
+                                          uint32_t step, int lane, bool valid, uint64_t dummy,
+                                          uint64_t lim = ~0ull) {
     static_assert(!(COPY && LINE), "MODE_COPY uses the 16-byte grid");
     const uint64_t base = rr.a0 & ~(Grid<LINE>::ALIGN - 1);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t k = step * (G * U) + u * G + lane;
-        const bool in = valid && k < nch;
+        const bool in = valid && k < nch && base + 16ull * k < lim;
         if constexpr (!COPY) {
             R.v[u] = ld16<NT>((gcv4)(in ? base + 16ull * k : dummy));
         } else {
@@ -287,14 +290,189 @@ __device__ __forceinline__ FieldLines field_lines(uint64_t a0, uint32_t fip, uin
     return f;
 }
 
+// The gates of one record (MODE_EMIT / MODE_VERIFY / MODE_COPY), run by its whole group once every
+// lane holds its part `acc` of the aligned-word sum over [0, span_end): the header bytes the lanes
+// summed are taken out again, the IPv4 header sum and the pseudo-header address words are read from
+// the LDS window (`winb`, record byte o at head + o), and lane 0 finishes and writes the record.
+template <int G, int MODE, bool IMPLICIT, bool LINE, class RD>
+__device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, uint32_t acc, const RD& rd,
+                                             const uint8_t* winb, uint32_t head, uint64_t a0, uint32_t len,
+                                             uint64_t r, int lane, u32x4* win, uint64_t base, uint32_t* gsh) {
+    constexpr bool COPY = MODE == MODE_COPY;
+    constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
+    constexpr int WIN = Grid<LINE>::WIN;
+    const bool odd = (a0 & 1u) != 0;
+    // Header bytes [0, l4_off) that the lanes summed (taken out of the L4 sum), the IPv4
+    // header's big-endian word sum and the pseudo-header address words.  All of them sit in
+    // the LDS window except behind a long Hop-by-Hop header (then read from global memory).
+    const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
+    const uint32_t l4_off = l4 ? g.l4_off : 0u;
+    uint32_t pre = 0;  // aligned-word sum contribution of the bytes [0, l4_off)
+    for (uint32_t i = lane; 2 * i < l4_off; i += G) {
+        // l4_off is even: record offset 2i is the low byte of an aligned little-endian
+        // word for an even record start, the high byte for an odd one
+        const uint32_t e = rd(2 * i), o = rd(2 * i + 1);
+        pre += odd ? ((e << 8) + o) : (e + (o << 8));
+    }
+    uint32_t hsum = 0, psum = 0;
+    if (g.fam == 4) {
+        for (uint32_t i = lane; i < g.ip_hl / 2; i += G) {
+            const uint32_t o = head + g.ip_off + 2 * i;
+            if (!(EMITS && i == 5)) hsum += (winb[o] << 8) | winb[o + 1];
+        }
+    }
+    if (l4 && (g.proto == P_UDP || g.proto == P_TCP || g.proto == P_ICMP6)) {
+        for (uint32_t i = lane; i < g.addr_words; i += G) {
+            const uint32_t o = head + g.addr_off + 2 * i;
+            psum += (winb[o] << 8) | winb[o + 1];
+        }
+    }
+    const uint32_t tot = group_sum<G>(acc);
+    pre = group_sum<G>(pre);
+    hsum = group_sum<G>(hsum);
+    psum = group_sum<G>(psum);
+    const gu8 wrec = (gu8)a0;
+    if (lane == 0) {
+        uint32_t st = g.st;
+        uint32_t fip = MF_NONE, fl4 = MF_NONE, vip = 0, vl4 = 0;  // emit: the field writes
+        // IPv4 header: data(header) (canonical fold of the big-endian word sum)
+        uint32_t ip_valid = 1, ip_ok = 1;
+        if (g.fam == 4) {
+            const uint32_t hdr = fold32(hsum);
+            if (EMITS) {
+                fip = g.ip_off + 10;
+                vip = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
+            } else {
+                ip_valid = hdr == 0xffffu;
+                ip_ok = caps_rx(p.caps_ipv4) ? ip_valid : 1u;
+            }
+        }
+        uint32_t l4_valid = 1, l4_ok = 1, partial = 0;
+        if (l4) {
+            const uint32_t fpos = g.l4_off + g.fo;
+            const uint32_t field = (rd(fpos) << 8) | rd(fpos + 1);
+            // aligned-word sum of the L4 span = lanes' sum of [0, span_end) minus the
+            // header bytes [0, l4_off) (exact: no u32 wrap below 131072 bytes)
+            uint32_t s = tot - pre;
+            if (EMITS) {
+                // the reference zeroes the field before summing: remove its bytes (the
+                // field offset is even: its parity is the record start's)
+                const uint32_t f0 = field >> 8, f1 = field & 0xffu;
+                s -= odd ? ((f0 << 8) + f1) : (f0 + (f1 << 8));
+            }
+            const uint32_t f = fold32(s);
+            const uint32_t dat = odd ? f : bswap16(f);  // == checksum::data(span)
+            uint32_t ph = 0, gate_caps = SMOL_CHECKSUM_NONE;
+            const bool pseudo = g.proto == P_UDP || g.proto == P_TCP || g.proto == P_ICMP6;
+            if (pseudo) {
+                const uint32_t plen = g.proto == P_UDP ? (g.span_end - g.l4_off) : g.l4_len;
+                ph = fold32(psum + g.proto + (plen & 0xffffu));  // pseudo_header()
+            }
+            const uint32_t comb = pseudo ? fold32(ph + dat) : dat;  // combine()
+            switch (g.proto) {
+                case P_UDP: gate_caps = p.caps_udp; break;
+                case P_TCP: gate_caps = p.caps_tcp; break;
+                case P_ICMP4: gate_caps = p.caps_icmpv4; break;
+                case P_ICMP6: gate_caps = p.caps_icmpv6; break;
+                default: gate_caps = SMOL_CHECKSUM_NONE; break;  // IGMP
+            }
+            if (EMITS) {
+                const bool fill = g.proto == P_IGMP ? true : caps_tx(gate_caps);
+                uint32_t c = ~comb & 0xffffu;
+                if (g.proto == P_UDP && c == 0) c = 0xffffu;  // udp.rs:207
+                fl4 = fpos;
+                vl4 = fill ? c : 0u;
+            } else {
+                l4_valid = comb == 0xffffu;
+                if (g.proto == P_UDP && field == 0) l4_valid = 1;  // udp.rs:138-140
+                if (g.proto == P_UDP || g.proto == P_TCP) partial = ph == field;
+                l4_ok = caps_rx(gate_caps) ? l4_valid : 1u;
+            }
+        }
+        if (EMITS) {
+            if (!COPY && p.patch) {
+                // two-pass emit: the fields are written by scatter_kernel after the read
+                // pass.  Fixed-stride batches on the line grid hand over whole 64-B lines
+                // when they lie in the window, inside the batch buffer and end inside
+                // this record (bytes before the record are the previous record's or the
+                // gap's; scatter_kernel checks the previous record's fields).
+                uint32_t lines = 0;
+                if (IMPLICIT && LINE && p.lines && p.stride >= 256 && (fip != MF_NONE || fl4 != MF_NONE)) {
+                    const FieldLines fl = field_lines(a0, fip, fl4);
+                    const uint64_t lend = fl.l0 + 64ull * fl.nl;
+                    if (fl.nl && fl.l0 >= (uint64_t)p.buf && lend <= a0 + len &&
+                        lend <= base + (uint64_t)WIN) {
+                        uint8_t* wb = reinterpret_cast<uint8_t*>(win);
+                        if (fip != MF_NONE) { wb[head + fip] = (uint8_t)(vip >> 8); wb[head + fip + 1] = (uint8_t)vip; }
+                        if (fl4 != MF_NONE) { wb[head + fl4] = (uint8_t)(vl4 >> 8); wb[head + fl4 + 1] = (uint8_t)vl4; }
+                        lines = (uint32_t)((fl.l0 - base) >> 4) | (fl.nl << 8);
+                    }
+                }
+                *gsh = lines;
+                ((GMEM uint64_t*)p.patch)[r] = (uint64_t)(fip | (lines ? MF_LINES : 0u)) |
+                                               ((uint64_t)fl4 << 16) | ((uint64_t)vip << 32) |
+                                               ((uint64_t)vl4 << 48);
+            } else {
+                if (fip != MF_NONE) store_be16(wrec + fip, vip);
+                if (fl4 != MF_NONE) store_be16(wrec + fl4, vl4);
+            }
+            if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
+        } else {
+            const bool mal = (st & SMOL_ST_MALFORMED) != 0;
+            st |= (ip_ok ? SMOL_ST_IP_OK : 0u) | (l4_ok ? SMOL_ST_L4_OK : 0u) |
+                  (partial ? SMOL_ST_L4_PARTIAL : 0u) | (ip_valid ? SMOL_ST_IP_VALID : 0u) |
+                  (l4_valid ? SMOL_ST_L4_VALID : 0u) |
+                  ((ip_ok && l4_ok && !mal) ? SMOL_ST_ACCEPT : 0u);
+            ((gu8)p.status)[r] = (uint8_t)st;
+        }
+    }
+    if constexpr (MODE == MODE_EMIT && IMPLICIT && LINE) {
+        if (p.patch && p.lines) {  // copy the patched line(s) from the window to the slot
+            wave_lds_sync();
+            const uint32_t lines = *gsh;
+#if defined(SMOL_EXP_NOSLOT)
+            const uint32_t nc = 0, c0 = lines & 0xffu;  // experiment: no slot copies
+#elif defined(SMOL_EXP_SLOT64)
+            const uint32_t nc = lines ? 4u : 0u, c0 = lines & 0xffu;  // experiment: one line only
+#else
+            const uint32_t nc = 4u * (lines >> 8), c0 = lines & 0xffu;
+#endif
+            for (uint32_t c = (uint32_t)lane; c < nc; c += G)
+                *(GMEM u32x4*)((uint64_t)p.lines + (uint64_t)LINE_SLOT * r + 16u * c) = win[c0 + c];
+        }
+    }
+}
+
+// Fixed-stride emit on the line grid: the 128-B line holding record r+1's first byte also holds
+// record r's last bytes, and with non-temporal loads two groups requesting it fetch it from HBM
+// twice (C2: 5.6 % more HBM reads than the records' bytes).  When the group of record r+1 is this
+// group's neighbour in the same wavefront, only that group loads the line — it is the first line of
+// its LDS window — and this group reads its tail chunks there.  Measured (tools/sweep.py): emit
+// 0.331 -> 0.304 ms on C2, 0.281 -> 0.263 ms on C4; verify got slower with it (C2 0.2377 -> 0.2434
+// ms, C4 0.2101 -> 0.2217 ms, although its HBM reads fell to the records' bytes), so verify keeps
+// loading both.  Returns the address
+// from which record r's chunks come from the neighbour's window (~0: none).  Records take 2 or 3
+// steps depending on their offset in the line, so groups are not in lockstep: the neighbour's
+// window is used only when record r+1 is the neighbour's one and only record (the natural grid),
+// so that it is filled at the start and never overwritten.  Stride >= 384 keeps that line out of
+// record r's own window.
+template <int G, int MODE, bool IMPLICIT, bool LINE>
+__device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, uint64_t a0, int gib, uint64_t ngroups) {
+    constexpr bool SHARE = IMPLICIT && LINE && MODE == MODE_EMIT;
+    constexpr int GPW = 64 / G;  // groups per wavefront
+    if (!SHARE || p.stride < 384 || (gib % GPW) == GPW - 1 || r + 1 >= p.n || r + 1 >= ngroups ||
+        r + 1 + ngroups < p.n)
+        return ~0ull;
+    return (a0 + p.stride) & ~127ull;
+}
+
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
-                                          uint32_t* gsh) {
+                                          uint32_t* gsh, int gib) {
     constexpr bool COPY = MODE == MODE_COPY;
-    constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
     constexpr int WIN = Grid<LINE>::WIN;
     constexpr int WIN_CH = Grid<LINE>::WIN_CH;
     static_assert(G * U >= WIN_CH, "step 0 must cover the LDS window");
@@ -308,7 +486,9 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     const uint32_t step2 = last ? 0u : w.step + 1;
     // SKIPD: no prefetch when the group has nothing left (one record per group in a natural grid:
     // every record's last step would otherwise issue U loads of the dummy line)
-    if (PF && (!SKIPD || have2)) load_step<G, U, NT, COPY, LINE>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy);
+    if (PF && (!SKIPD || have2))
+        load_step<G, U, NT, COPY, LINE>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
+                                        shared_from<G, MODE, IMPLICIT, LINE>(p, r2, rec2.a0, gib, ngroups));
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
@@ -412,12 +592,14 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 
     // ---- sum this step's chunks over [0, s1) (data: [0, len)) ----
     const int s1 = w.s1;
+    const uint64_t lim = shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t k = w.step * (G * U) + u * G + lane;
         const int pos = (int)(16u * k) - (int)head;  // chunk start relative to the record
         if (k < w.nch && pos < s1 && pos + 16 > 0) {
-            const u32x4 c = cm[u];
+            const uint64_t ca = base + 16ull * k;
+            const u32x4 c = ca >= lim ? win[WIN_CH + ((ca - lim) >> 4)] : cm[u];  // neighbour's window
             if (pos < 0 || pos + 16 > s1) {  // first chunk (bytes before the record) / tail
                 if (MODE == MODE_DATA) {
                     const int lo = -pos, hi = s1 - pos;
@@ -448,146 +630,8 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const uint32_t tot = group_sum<G>(s_rel);
             if (lane == 0) ((gu16)p.out16)[r] = (uint16_t)bswap16(fold32(tot));
         } else {
-            const Geom& g = w.g;
-            // Header bytes [0, l4_off) that the lanes summed (taken out of the L4 sum), the IPv4
-            // header's big-endian word sum and the pseudo-header address words.  All of them sit in
-            // the LDS window except behind a long Hop-by-Hop header (then read from global memory).
-            const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
-            const uint32_t l4_off = l4 ? g.l4_off : 0u;
-            uint32_t pre = 0;  // aligned-word sum contribution of the bytes [0, l4_off)
-            for (uint32_t i = lane; 2 * i < l4_off; i += G) {
-                // l4_off is even: record offset 2i is the low byte of an aligned little-endian
-                // word for an even record start, the high byte for an odd one
-                const uint32_t e = rd(2 * i), o = rd(2 * i + 1);
-                pre += odd ? ((e << 8) + o) : (e + (o << 8));
-            }
-            uint32_t hsum = 0, psum = 0;
-            if (g.fam == 4) {
-                for (uint32_t i = lane; i < g.ip_hl / 2; i += G) {
-                    const uint32_t o = head + g.ip_off + 2 * i;
-                    if (!(EMITS && i == 5)) hsum += (winb[o] << 8) | winb[o + 1];
-                }
-            }
-            if (l4 && (g.proto == P_UDP || g.proto == P_TCP || g.proto == P_ICMP6)) {
-                for (uint32_t i = lane; i < g.addr_words; i += G) {
-                    const uint32_t o = head + g.addr_off + 2 * i;
-                    psum += (winb[o] << 8) | winb[o + 1];
-                }
-            }
-            const uint32_t tot = group_sum<G>(w.acc);
-            pre = group_sum<G>(pre);
-            hsum = group_sum<G>(hsum);
-            psum = group_sum<G>(psum);
-            const gu8 wrec = (gu8)w.cur.a0;
-            if (lane == 0) {
-                uint32_t st = g.st;
-                uint32_t fip = MF_NONE, fl4 = MF_NONE, vip = 0, vl4 = 0;  // emit: the field writes
-                // IPv4 header: data(header) (canonical fold of the big-endian word sum)
-                uint32_t ip_valid = 1, ip_ok = 1;
-                if (g.fam == 4) {
-                    const uint32_t hdr = fold32(hsum);
-                    if (EMITS) {
-                        fip = g.ip_off + 10;
-                        vip = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
-                    } else {
-                        ip_valid = hdr == 0xffffu;
-                        ip_ok = caps_rx(p.caps_ipv4) ? ip_valid : 1u;
-                    }
-                }
-                uint32_t l4_valid = 1, l4_ok = 1, partial = 0;
-                if (l4) {
-                    const uint32_t fpos = g.l4_off + g.fo;
-                    const uint32_t field = (rd(fpos) << 8) | rd(fpos + 1);
-                    // aligned-word sum of the L4 span = lanes' sum of [0, span_end) minus the
-                    // header bytes [0, l4_off) (exact: no u32 wrap below 131072 bytes)
-                    uint32_t s = tot - pre;
-                    if (EMITS) {
-                        // the reference zeroes the field before summing: remove its bytes (the
-                        // field offset is even: its parity is the record start's)
-                        const uint32_t f0 = field >> 8, f1 = field & 0xffu;
-                        s -= odd ? ((f0 << 8) + f1) : (f0 + (f1 << 8));
-                    }
-                    const uint32_t f = fold32(s);
-                    const uint32_t dat = odd ? f : bswap16(f);  // == checksum::data(span)
-                    uint32_t ph = 0, gate_caps = SMOL_CHECKSUM_NONE;
-                    const bool pseudo = g.proto == P_UDP || g.proto == P_TCP || g.proto == P_ICMP6;
-                    if (pseudo) {
-                        const uint32_t plen = g.proto == P_UDP ? (g.span_end - g.l4_off) : g.l4_len;
-                        ph = fold32(psum + g.proto + (plen & 0xffffu));  // pseudo_header()
-                    }
-                    const uint32_t comb = pseudo ? fold32(ph + dat) : dat;  // combine()
-                    switch (g.proto) {
-                        case P_UDP: gate_caps = p.caps_udp; break;
-                        case P_TCP: gate_caps = p.caps_tcp; break;
-                        case P_ICMP4: gate_caps = p.caps_icmpv4; break;
-                        case P_ICMP6: gate_caps = p.caps_icmpv6; break;
-                        default: gate_caps = SMOL_CHECKSUM_NONE; break;  // IGMP
-                    }
-                    if (EMITS) {
-                        const bool fill = g.proto == P_IGMP ? true : caps_tx(gate_caps);
-                        uint32_t c = ~comb & 0xffffu;
-                        if (g.proto == P_UDP && c == 0) c = 0xffffu;  // udp.rs:207
-                        fl4 = fpos;
-                        vl4 = fill ? c : 0u;
-                    } else {
-                        l4_valid = comb == 0xffffu;
-                        if (g.proto == P_UDP && field == 0) l4_valid = 1;  // udp.rs:138-140
-                        if (g.proto == P_UDP || g.proto == P_TCP) partial = ph == field;
-                        l4_ok = caps_rx(gate_caps) ? l4_valid : 1u;
-                    }
-                }
-                if (EMITS) {
-                    if (!COPY && p.patch) {
-                        // two-pass emit: the fields are written by scatter_kernel after the read
-                        // pass.  Fixed-stride batches on the line grid hand over whole 64-B lines
-                        // when they lie in the window, inside the batch buffer and end inside
-                        // this record (bytes before the record are the previous record's or the
-                        // gap's; scatter_kernel checks the previous record's fields).
-                        uint32_t lines = 0;
-                        if (IMPLICIT && LINE && p.lines && p.stride >= 256 && (fip != MF_NONE || fl4 != MF_NONE)) {
-                            const FieldLines fl = field_lines(w.cur.a0, fip, fl4);
-                            const uint64_t lend = fl.l0 + 64ull * fl.nl;
-                            if (fl.nl && fl.l0 >= (uint64_t)p.buf && lend <= w.cur.a0 + w.cur.len &&
-                                lend <= base + (uint64_t)WIN) {
-                                uint8_t* wb = reinterpret_cast<uint8_t*>(win);
-                                if (fip != MF_NONE) { wb[head + fip] = (uint8_t)(vip >> 8); wb[head + fip + 1] = (uint8_t)vip; }
-                                if (fl4 != MF_NONE) { wb[head + fl4] = (uint8_t)(vl4 >> 8); wb[head + fl4 + 1] = (uint8_t)vl4; }
-                                lines = (uint32_t)((fl.l0 - base) >> 4) | (fl.nl << 8);
-                            }
-                        }
-                        *gsh = lines;
-                        ((GMEM uint64_t*)p.patch)[r] = (uint64_t)(fip | (lines ? MF_LINES : 0u)) |
-                                                       ((uint64_t)fl4 << 16) | ((uint64_t)vip << 32) |
-                                                       ((uint64_t)vl4 << 48);
-                    } else {
-                        if (fip != MF_NONE) store_be16(wrec + fip, vip);
-                        if (fl4 != MF_NONE) store_be16(wrec + fl4, vl4);
-                    }
-                    if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
-                } else {
-                    const bool mal = (st & SMOL_ST_MALFORMED) != 0;
-                    st |= (ip_ok ? SMOL_ST_IP_OK : 0u) | (l4_ok ? SMOL_ST_L4_OK : 0u) |
-                          (partial ? SMOL_ST_L4_PARTIAL : 0u) | (ip_valid ? SMOL_ST_IP_VALID : 0u) |
-                          (l4_valid ? SMOL_ST_L4_VALID : 0u) |
-                          ((ip_ok && l4_ok && !mal) ? SMOL_ST_ACCEPT : 0u);
-                    ((gu8)p.status)[r] = (uint8_t)st;
-                }
-            }
-            if constexpr (MODE == MODE_EMIT && IMPLICIT && LINE) {
-                if (p.patch && p.lines) {  // copy the patched line(s) from the window to the slot
-                    wave_lds_sync();
-                    const uint32_t lines = *gsh;
-#if defined(SMOL_EXP_NOSLOT)
-                    const uint32_t nc = 0, c0 = lines & 0xffu;  // experiment: no slot copies
-#elif defined(SMOL_EXP_SLOT64)
-                    const uint32_t nc = lines ? 4u : 0u, c0 = lines & 0xffu;  // experiment: one line only
-#else
-                    const uint32_t nc = 4u * (lines >> 8), c0 = lines & 0xffu;
-#endif
-                    for (uint32_t c = (uint32_t)lane; c < nc; c += G)
-                        *(GMEM u32x4*)((uint64_t)p.lines + (uint64_t)LINE_SLOT * r + 16u * c) = win[c0 + c];
-                }
-            }
+            finish_gates<G, MODE, IMPLICIT, LINE>(p, w.g, w.acc, rd, winb, head, w.cur.a0, w.cur.len, r, lane, win,
+                                                  base, gsh);
         }
     }
 
@@ -637,16 +681,18 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     Regs<U, COPY> va;
     if (PF) {
         Regs<U, COPY> vb;
-        load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy);
+        load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
+                                        shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, va, vb, lane, ngroups, &win[gib][0], &gsh[gib])) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, vb, va, lane, ngroups, &win[gib][0], &gsh[gib])) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, va, vb, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, vb, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
         }
     } else {
         while (true) {
-            load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy);
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, va, va, lane, ngroups, &win[gib][0], &gsh[gib])) break;
+            load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
+                                            shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, va, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
         }
     }
 }

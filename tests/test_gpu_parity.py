@@ -522,7 +522,7 @@ def test_emit_two_pass_neighbour_fields(eng):
         for off in (0, 5, 40, 63):
             host = np.concatenate([rng.integers(0, 256, off, dtype=np.uint8),
                                    np.frombuffer(b"".join(recs), np.uint8), np.zeros(128, np.uint8)])
-            for variant, defer in [(-1, None), (5, 1), (6, 1), (1, 1)]:
+            for variant, defer in [(-1, None), (5, 1), (6, 1), (1, 1), (0, 0), (5, 0)]:
                 _emit_case(eng, host, off, n, stride, stride, E.KIND_IP, CAPS_DEFAULT, variant, defer)
 
 

@@ -13,18 +13,12 @@ step() {  # step <name> <seconds> <cmd...>: stop on the first failure
     if [ $rc -ne 0 ]; then tail -30 "$O/$name.log"; exit $rc; fi
     tail -${TAILN:-1} "$O/$name.log"
 }
-kstats() {
-    python3 - $1 <<'PY'
-import csv, glob, sys
-f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
-for r in csv.DictReader(open(f)):
-    if "csum" in r["Name"] or "scatter" in r["Name"]:
-        print("   ", r["Name"][:70], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
-PY
-}
-for lib in default NOSLOT SLOT64; do
-    L=smoltcp_amd/libsmolcsum.so; [ $lib != default ] && L=build_alt/lib_$lib.so
-    SMOLCSUM_LIB=$L step kt_$lib 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$lib -o run -- python3 bench.py --config c2 --steps 20 --cpu-seconds 0 --variant 5 --defer 1 --shape 7
-    kstats $O/kt_$lib
+TAILN=3 step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+for lib in default NOSHARE; do
+L=smoltcp_amd/libsmolcsum.so; [ $lib != default ] && L=build_alt/lib_$lib.so
+for c in c2 c4; do
+    SMOLCSUM_LIB=$L TAILN=0 step sweep_${c}_$lib 600 python tools/sweep.py --config $c --shapes 0,7 --var 1,5 --defer 0
+    grep '"round": 1' $O/sweep_${c}_$lib.log | cut -c1-140
+done
 done
 echo "== done"

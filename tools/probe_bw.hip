@@ -137,6 +137,40 @@ __global__ __launch_bounds__(256) void rec_walk(const uint8_t* __restrict__ buf,
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// Stripe access: each wave reads R consecutive 1500-B records as one line-aligned contiguous
+// region (1 KiB per load instruction across the wave), natural grid (one stripe per wave).
+// LDS=true also stages every chunk through LDS (ds_write_b128 + ds_read_b128 by another lane).
+template <int R, bool NT, bool LDS>
+__global__ __launch_bounds__(256) void stripe(const uint8_t* __restrict__ buf, uint64_t n, uint32_t* sink) {
+    constexpr int U = (R * 1500 + 127 + 1023) / 1024;
+    __shared__ uint4 st[LDS ? 4 * 64 * U : 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t r0 = ((uint64_t)blockIdx.x * 4 + wv) * R;
+    if (r0 >= n) return;
+    const uint64_t a0 = (uint64_t)buf + r0 * 1500;
+    const uint64_t base = a0 & ~127ull;
+    const uint64_t rn = r0 + R < n ? r0 + R : n;
+    const uint64_t end = (uint64_t)buf + rn * 1500;
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t q = base + 16ull * (u * 64 + lane);
+        const uint4* pq = (const uint4*)(q < end ? q : (uint64_t)buf);
+        v[u] = NT ? ldnt(pq) : *pq;
+    }
+    uint32_t acc = 0;
+    if (LDS) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) st[(wv * U + u) * 64 + lane] = v[u];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = st[(wv * U + u) * 64 + (lane ^ 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += __builtin_amdgcn_sad_u16(v[u].x, 0, 0) + __builtin_amdgcn_sad_u16(v[u].y, 0, 0) + __builtin_amdgcn_sad_u16(v[u].z, 0, 0) + __builtin_amdgcn_sad_u16(v[u].w, 0, 0);
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const uint64_t bytes = argc > 1 ? strtoull(argv[1], 0, 0) : 1572864000ull;
     const uint64_t n16 = bytes / 16;
@@ -190,6 +224,13 @@ int main(int argc, char** argv) {
         recrun("rec_walk G16U4 nt line", rec_walk<16, 4, true, true>, 16);
         recrun("rec_walk G64U2 nt line", rec_walk<64, 2, true, true>, 64);
         recrun("rec_walk G64U2 plain 16B", rec_walk<64, 2, false, false>, 64);
+        // stripes: one wave per R records, 4 R records per block (recrun's 256 / G = 4 R)
+        recrun("stripe R8 nt", stripe<8, true, false>, 8);
+        recrun("stripe R8 plain", stripe<8, false, false>, 8);
+        recrun("stripe R8 nt LDS", stripe<8, true, true>, 8);
+        recrun("stripe R16 nt", stripe<16, true, false>, 4);
+        recrun("stripe R4 nt", stripe<4, true, false>, 16);
+        recrun("stripe R4 nt LDS", stripe<4, true, true>, 16);
     }
     CK(hipFree(p));
         return 0;
