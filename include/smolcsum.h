@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SMOLCSUM_ABI_VERSION 1
+#define SMOLCSUM_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------------------------ */
 enum {
@@ -164,10 +164,10 @@ typedef struct smol_csum_ctx smol_csum_ctx_t;
 int smol_csum_ctx_create(int device, smol_csum_ctx_t** out);
 int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx);
 
-/* Reserve the deferred-emit workspace for batches of up to `max_records` records (8 bytes per
- * record, capped at 2^23 records; larger batches are processed in chunks).  Only needed with the
- * deferred emit (smolcsum_tools.h): its first call would otherwise allocate device memory, which
- * must not happen inside a HIP graph capture. */
+/* Reserve the two-pass emit workspace for batches of up to `max_records` records (136 bytes per
+ * record, capped at 2^20 records; larger batches are processed in chunks).  Only needed with the
+ * two-pass emit (smol_csum_tool_set_deferred_emit): its first call would otherwise allocate
+ * device memory, which must not happen inside a HIP graph capture. */
 int smol_csum_ctx_reserve(smol_csum_ctx_t* ctx, uint64_t max_records);
 
 /* checksum::data() over every record span; d_out[i] = data(record i) (u16, numeric value as the
@@ -208,6 +208,38 @@ typedef struct {
 int smol_csum_batch_copy_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                               const uint8_t* d_src, const smol_csum_copy_t* d_copy,
                               const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
+
+/* ---- 3. 6LoWPAN next-header-compressed UDP (RFC 6282 §4.3) ------------------------------- */
+
+/* The IPv6 source and destination addresses of one record (32 bytes, device memory): 6LoWPAN's
+ * IPHC header compresses them (to nothing, when they derive from the link-layer addresses), so the
+ * iface's decompression result travels beside the batch. */
+typedef struct {
+    uint8_t src[16];
+    uint8_t dst[16];
+} smol_ipv6_addr_pair_t;
+
+/* UdpNhcRepr::emit's checksum (src/wire/sixlowpan/nhc.rs:746-776) over every record: each record
+ * is a LOWPAN_NHC UDP packet, from its dispatch byte (0b11110CPP) to the end of the payload; the
+ * payload follows an inline checksum (UdpNhcPacket::payload_mut, nhc.rs:622-626).  Under
+ * caps.udp.tx() the checksum !combine([pseudo_header_v6(src, dst, Udp, n + 8), src_port,
+ * dst_port, n + 8, data(payload)]) is written to the field and the C bit cleared (set_checksum,
+ * nhc.rs:676-681; no 0 -> 0xffff mapping); otherwise nothing is written.  The ports are read back
+ * from the packet in the encoding set_ports (nhc.rs:635-673) wrote them.  A record shorter than
+ * its header or without the UDP dispatch is left untouched and reported SMOL_ST_MALFORMED.
+ * `d_addrs` holds n address pairs (4-byte aligned); record kinds are ignored. */
+int smol_csum_batch_nhc_udp_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
+                                 const smol_ipv6_addr_pair_t* d_addrs, const smol_checksum_caps_t* caps,
+                                 uint8_t* d_status, void* stream);
+
+/* UdpNhcRepr::parse's checksum gate (src/wire/sixlowpan/nhc.rs:693-729): SMOL_ST_MALFORMED when
+ * UdpNhcPacket::check_len (nhc.rs:486-500) or the dispatch test fails; otherwise under
+ * caps.udp.rx() an inline checksum must equal the one computed over the ports as the packet
+ * accessors read them (nhc.rs:513-577); an elided checksum (C bit set) is not checked.  The IP
+ * bits are always set (no IPv4 header). */
+int smol_csum_batch_nhc_udp_verify(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
+                                   const smol_csum_batch_t* batch, const smol_ipv6_addr_pair_t* d_addrs,
+                                   const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
 
 /* Message of the last SMOL_EHIP error on this thread ("" if none). */
 const char* smol_csum_last_error(void);

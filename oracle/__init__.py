@@ -104,6 +104,15 @@ def lib() -> ctypes.CDLL:
     L.oracle_batch_copy_emit.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                          ctypes.c_uint8, ctypes.POINTER(CapsC), u8p, u8p, u8p]
     L.oracle_batch_copy_emit.restype = None
+    L.oracle_nhc_udp_verify.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.POINTER(CapsC)]
+    L.oracle_nhc_udp_verify.restype = ctypes.c_uint8
+    L.oracle_nhc_udp_emit.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.POINTER(CapsC)]
+    L.oracle_nhc_udp_emit.restype = ctypes.c_uint8
+    for name in ("oracle_batch_nhc_udp_emit", "oracle_batch_nhc_udp_verify"):
+        f = getattr(L, name)
+        f.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, u8p,
+                      ctypes.POINTER(CapsC), u8p]
+        f.restype = None
     _LIB = L
     return L
 
@@ -164,4 +173,29 @@ def batch_verify(buf: np.ndarray, desc, n: int, stride: int = 0, length: int = 0
     c = caps_c(caps)
     lib().oracle_batch_verify(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride,
                               length, kind, ctypes.byref(c), _ptr(st))
+    return st
+
+
+def batch_nhc_udp_emit(buf: np.ndarray, desc, n: int, addrs: np.ndarray, stride: int = 0, length: int = 0,
+                       caps=(0, 0, 0, 0, 0)):
+    """6LoWPAN NHC UDP emit (nhc.rs:746-776) in place on ``buf``; ``addrs``: n x 32 bytes (src, dst).
+    Returns the status array."""
+    st = np.zeros(n, dtype=np.uint8)
+    c = caps_c(caps)
+    addrs = np.ascontiguousarray(addrs, dtype=np.uint8)
+    assert addrs.size >= 32 * n
+    lib().oracle_batch_nhc_udp_emit(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride, length,
+                                    _ptr(addrs), ctypes.byref(c), _ptr(st))
+    return st
+
+
+def batch_nhc_udp_verify(buf: np.ndarray, desc, n: int, addrs: np.ndarray, stride: int = 0, length: int = 0,
+                         caps=(0, 0, 0, 0, 0)):
+    """6LoWPAN NHC UDP parse gate (nhc.rs:693-729); returns the status array."""
+    st = np.zeros(n, dtype=np.uint8)
+    c = caps_c(caps)
+    addrs = np.ascontiguousarray(addrs, dtype=np.uint8)
+    assert addrs.size >= 32 * n
+    lib().oracle_batch_nhc_udp_verify(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride, length,
+                                      _ptr(addrs), ctypes.byref(c), _ptr(st))
     return st

@@ -133,3 +133,64 @@ def icmpv6_fill(p: bytearray, src: bytes, dst: bytes) -> None:
     """src/wire/icmpv6.rs:538-553."""
     fill_l4(p, 2, 0)
     fill_l4(p, 2, ~combine([pseudo_header_v6(src, dst, 58, len(p)), data(bytes(p))]) & 0xFFFF)
+
+
+# ---- 6LoWPAN NHC UDP (src/wire/sixlowpan/nhc.rs) -----------------------------------------------
+
+
+def _nhc_sizes(b0: int):
+    """UdpNhcPacket::ports_size / checksum_size, nhc.rs:593-611."""
+    ports = {0: 4, 1: 3, 2: 3, 3: 1}[b0 & 3]
+    return ports, (0 if b0 & 4 else 2)
+
+
+def nhc_ports(p: bytes, emit: bool = False):
+    """src_port / dst_port accessors (nhc.rs:513-577) as written; with ``emit`` the destination of
+    mode 0b01 comes from byte 3, where set_ports (nhc.rs:655-662) put it."""
+    m = p[0] & 3
+    src = (p[1] << 8 | p[2]) if m in (0, 1) else (0xF000 + p[1]) if m == 2 else 0xF0B0 + (p[1] >> 4)
+    if m == 0:
+        dst = p[3] << 8 | p[4]
+    elif m == 1:
+        dst = 0xF000 + (p[3] if emit else p[1])
+    elif m == 2:
+        dst = p[2] << 8 | p[3]
+    else:
+        dst = 0xF0B0 + p[1]
+    return src, dst
+
+
+def nhc_udp_checksum(src: bytes, dst: bytes, sport: int, dport: int, payload: bytes) -> int:
+    """nhc.rs:705-716 / :760-771."""
+    n = len(payload)
+    return ~combine([pseudo_header_v6(src, dst, 17, n + 8), sport, dport, (n + 8) & 0xFFFF,
+                     data(payload)]) & 0xFFFF
+
+
+def nhc_udp_verify(p: bytes, src: bytes, dst: bytes):
+    """UdpNhcRepr::parse's checksum test (nhc.rs:697-723): None when the packet is dropped before
+    it (check_len, dispatch), else whether the inline checksum (if any) matches."""
+    if len(p) < 1:
+        return None
+    ports, cs = _nhc_sizes(p[0])
+    if 1 + ports + cs > len(p) or (p[0] >> 3) != 0x1E:
+        return None
+    if cs == 0:
+        return True
+    sport, dport = nhc_ports(p)
+    return nhc_udp_checksum(src, dst, sport, dport, p[1 + ports + cs:]) == (p[1 + ports] << 8 | p[2 + ports])
+
+
+def nhc_udp_fill(p: bytearray, src: bytes, dst: bytes) -> bool:
+    """UdpNhcRepr::emit's checksum (nhc.rs:759-774): payload after an inline checksum, C bit
+    cleared, field written.  False (untouched) when the header does not fit / no UDP dispatch."""
+    if len(p) < 1:
+        return False
+    ports, _ = _nhc_sizes(p[0])
+    if 1 + ports + 2 > len(p) or (p[0] >> 3) != 0x1E:
+        return False
+    sport, dport = nhc_ports(bytes(p), emit=True)
+    c = nhc_udp_checksum(src, dst, sport, dport, bytes(p[1 + ports + 2:]))
+    p[0] &= ~4 & 0xFF
+    fill_l4(p, 1 + ports, c)
+    return True

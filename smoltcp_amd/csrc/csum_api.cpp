@@ -20,7 +20,7 @@ struct smol_csum_ctx {
     int num_cu;
     uint32_t max_blocks;  // grid cap (kNaturalGrid: one work item per group)
     int shape;            // -1 automatic, else CFG_*
-    int variant;          // kernel variant (-1 automatic; csum_kernels.hip VarT, 3/4 tile kernel)
+    int variant;          // kernel variant (-1 automatic; csum_walk.h VarT, 3/4 tile kernel)
     uint8_t* dummy;       // 256 zero bytes on the device (target of loads with nothing to read)
     int defer_emit;       // -1 automatic, 0 field stores in the read pass, 1 two-pass emit
     uint64_t* patch;      // two-pass emit workspace: one meta word per record of a chunk
@@ -144,7 +144,8 @@ int reserve_patch(smol_csum_ctx_t* ctx, uint64_t n) {
 
 int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t* b,
         const smol_checksum_caps_t* caps, uint16_t* d_out, uint8_t* d_status, void* stream,
-        const uint8_t* d_src = nullptr, const smol_csum_copy_t* d_copy = nullptr) {
+        const uint8_t* d_src = nullptr, const smol_csum_copy_t* d_copy = nullptr,
+        const uint8_t* d_addrs = nullptr) {
     KParams p;
     std::memset(&p, 0, sizeof p);
     p.src = d_src;
@@ -154,7 +155,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.n = b->n;
     p.stride = b->stride;
     p.len = b->len;
-    p.kind = b->kind;
+    p.kind = d_addrs ? KIND_NHC_UDP : b->kind;
+    p.addrs = d_addrs;
     if (caps) {
         p.caps_ipv4 = caps->ipv4;
         p.caps_udp = caps->udp;
@@ -168,17 +170,18 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.num_cu = ctx->max_blocks_set ? 0u : (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
-    // Variants: 0-2, 5-6 = walk kernel (csum_kernels.hip VarT: load policy, prefetch, chunk
+    // Variants: 0-2, 5-6 = walk kernel (csum_walk.h VarT: load policy, prefetch, chunk
     // grid), 3-4 = tile kernel (csum_tile.hip: nt / plain loads), emit and verify only.
     int variant = ctx->variant;
     if (variant < 0) variant = auto_variant(mode, b->desc != nullptr);
     if (mode == MODE_DATA && (variant == 3 || variant == 4)) variant = 0;
+    if (d_addrs && (variant == 3 || variant == 4)) variant = auto_variant(mode, b->desc != nullptr);  // walk only
     const bool use_tile = variant == 3 || variant == 4;
     int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr, line_grid(variant));
     // Two-pass emit only on request: it trades the in-pass 2-byte stores for a meta word + line
     // slot per record and a scatter pass, and measured slower (C2: read pass 0.301 ms + scatter
     // 0.047 ms against 0.315 ms in one pass; the slot writes alone cost 0.049 ms).
-    const bool two_pass = ctx->defer_emit == 1;
+    const bool two_pass = ctx->defer_emit == 1 && !d_addrs;
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
         hipError_t e = launch_csum(MODE_COPY, shape, 1, p, ctx->max_blocks, s);
@@ -374,6 +377,30 @@ int smol_csum_batch_copy_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_c
     if (rc != SMOL_OK || b->n == 0) return rc;
     if (!d_src || !d_copy || ((uintptr_t)d_copy & 15u) != 0) return SMOL_EINVAL;
     return run(ctx, MODE_COPY, d_buf, b, caps, nullptr, d_status, stream, d_src, d_copy);
+}
+
+// ---- 6LoWPAN NHC UDP --------------------------------------------------------------------------
+
+int smol_csum_batch_nhc_udp_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* b,
+                                 const smol_ipv6_addr_pair_t* d_addrs, const smol_checksum_caps_t* caps,
+                                 uint8_t* d_status, void* stream) {
+    if (!ctx || !caps_valid(caps)) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK || b->n == 0) return rc;
+    if (!d_addrs || ((uintptr_t)d_addrs & 3u) != 0) return SMOL_EINVAL;
+    return run(ctx, MODE_EMIT, d_buf, b, caps, nullptr, d_status, stream, nullptr, nullptr,
+               reinterpret_cast<const uint8_t*>(d_addrs));
+}
+
+int smol_csum_batch_nhc_udp_verify(smol_csum_ctx_t* ctx, const uint8_t* d_buf, const smol_csum_batch_t* b,
+                                   const smol_ipv6_addr_pair_t* d_addrs, const smol_checksum_caps_t* caps,
+                                   uint8_t* d_status, void* stream) {
+    if (!ctx || !caps_valid(caps)) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK || b->n == 0) return rc;
+    if (!d_status || !d_addrs || ((uintptr_t)d_addrs & 3u) != 0) return SMOL_EINVAL;
+    return run(ctx, MODE_VERIFY, const_cast<uint8_t*>(d_buf), b, caps, nullptr, d_status, stream, nullptr,
+               nullptr, reinterpret_cast<const uint8_t*>(d_addrs));
 }
 
 const char* smol_csum_last_error(void) { return g_last_error.c_str(); }

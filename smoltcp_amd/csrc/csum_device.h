@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "../../include/smolcsum.h"
+#include "csum_launch.h"
 
 namespace smolcsum {
 
@@ -56,7 +57,7 @@ __device__ __forceinline__ bool caps_tx(uint32_t c) {  // Checksum::tx, src/phy/
     return c == SMOL_CHECKSUM_BOTH || c == SMOL_CHECKSUM_TX;
 }
 
-enum : uint32_t { P_NONE = 0, P_ICMP4 = 1, P_IGMP = 2, P_TCP = 6, P_UDP = 17, P_ICMP6 = 58 };
+enum : uint32_t { P_NONE = 0, P_ICMP4 = 1, P_IGMP = 2, P_TCP = 6, P_UDP = 17, P_ICMP6 = 58, P_NHC_UDP = 0x111 };
 
 // Where the gates of one record look.  Offsets are relative to the record start.
 struct Geom {
@@ -70,7 +71,7 @@ struct Geom {
     uint32_t l4_off;     // L4 buffer offset (the slice the reference wraps in the L4 Packet)
     uint32_t l4_len;     // L4 buffer length
     uint32_t span_end;   // end of the summed L4 span (UDP: l4_off + UDP length field)
-    uint32_t fo;         // checksum field offset inside the L4 header
+    uint32_t fo;         // checksum field offset inside the L4 header (NHC UDP: in the record)
 };
 
 // Record geometry: how smoltcp's iface reaches the checksum gates.  Mirrors, check for check,
@@ -83,11 +84,29 @@ struct Geom {
 //   L4        UdpPacket::check_len udp.rs:57-69, TcpPacket::check_len tcp.rs:155-167,
 //             Icmpv4Packet::check_len icmpv4.rs:207-214, IgmpPacket::check_len igmp.rs:73-80,
 //             the generic len >= 4 of Icmpv6Packet::check_len icmpv6.rs:275-280.
+//   6LoWPAN NHC UDP (KIND_NHC_UDP): UdpNhcPacket::check_len nhc.rs:486-500 and the dispatch test of
+//             UdpNhcRepr::parse :701-703; the payload follows the inline checksum if any, and on
+//             emit always an inline checksum (payload_mut :622-626).
 // `rd(o)` returns the record byte at offset o (only called for o < len).
-template <class RD>
-__device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint32_t kind) {
+// NHC: the instantiation for the 6LoWPAN entry points (the IP path carries no NHC code).
+template <bool NHC = false, class RD>
+__device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint32_t kind, bool emit = false) {
     Geom g = {};
     uint32_t ip_off = 0;
+    if (NHC && kind == KIND_NHC_UDP) {
+        if (len < 1) { g.st = SMOL_ST_MALFORMED; return g; }
+        const uint32_t b0 = rd(0);
+        const uint32_t ps = (b0 & 3u) == 0 ? 4u : (b0 & 3u) == 3 ? 1u : 3u;  // ports_size :602-611
+        const uint32_t cs = (emit || !(b0 & 4u)) ? 2u : 0u;                     // checksum_size :593-599
+        if (1 + ps + cs > len || (b0 >> 3) != 0x1eu) { g.st = SMOL_ST_MALFORMED; return g; }
+        g.proto = P_NHC_UDP;
+        g.l4_off = 1 + ps + cs;
+        g.l4_len = len - g.l4_off;
+        g.span_end = len;
+        g.fo = 1 + ps;
+        g.addr_words = 16;
+        return g;
+    }
     if (kind == SMOL_KIND_ETH) {
         if (len < 14) { g.st = SMOL_ST_MALFORMED; return g; }
         uint32_t et = (rd(12) << 8) | rd(13);

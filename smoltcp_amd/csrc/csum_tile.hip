@@ -13,7 +13,7 @@
 //      trailing bytes past the L4 span), and applies the gate: status byte (verify) or field
 //      writes (emit).  64 records per instruction instead of one record per group-instruction.
 //
-// The previous design (csum_kernels.hip: a group parses and finishes its own record) spent
+// The walk kernel (csum_walk.h: a group parses and finishes its own record) spent
 // ~134 VALU + ~68 SALU wave-instructions per 1500-byte record (rocprofv3 SQ_INSTS_*); here
 // phase B is a short straight loop and phase C is fully SIMD-parallel.
 //

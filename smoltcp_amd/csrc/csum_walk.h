@@ -92,7 +92,7 @@ struct RecRef {
 
 constexpr uint32_t KIND_BAD_COPY = 0x100;
 
-template <bool IMPLICIT, bool COPY>
+template <bool IMPLICIT, bool COPY, bool NHC = false>
 __device__ __forceinline__ RecRef rec_at(const KParams& p, uint64_t r) {
     RecRef rr;
     if (IMPLICIT) {
@@ -103,7 +103,7 @@ __device__ __forceinline__ RecRef rec_at(const KParams& p, uint64_t r) {
         const u32x4 d = *(gcv4)((uint64_t)p.desc + 16 * r);
         rr.a0 = (uint64_t)p.buf + ((uint64_t)d.x | ((uint64_t)d.y << 32));
         rr.len = d.z;
-        rr.kind = d.w & 0xffu;
+        rr.kind = NHC ? KIND_NHC_UDP : (d.w & 0xffu);  // NHC UDP entry points: every record
     }
     rr.sb = 0;
     rr.p0 = rr.p1 = 0;
@@ -210,6 +210,13 @@ __device__ __forceinline__ uint32_t ld_byte_sync(uint64_t a) {
     return x;
 }
 
+// The same for one aligned dword (the IPv6 addresses of 6LoWPAN NHC UDP records).
+__device__ __forceinline__ uint32_t ld_u32_sync(uint64_t a) {
+    uint32_t x;
+    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(a) : "memory");
+    return x;
+}
+
 // Sum over the G lanes of a group (all of them active).  Rows of 16 lanes reduce with DPP
 // (quad_perm xor1 / xor2, row_half_mirror, row_mirror), wider groups add ds_swizzle / bpermute.
 template <int G>
@@ -294,7 +301,7 @@ __device__ __forceinline__ FieldLines field_lines(uint64_t a0, uint32_t fip, uin
 // lane holds its part `acc` of the aligned-word sum over [0, span_end): the header bytes the lanes
 // summed are taken out again, the IPv4 header sum and the pseudo-header address words are read from
 // the LDS window (`winb`, record byte o at head + o), and lane 0 finishes and writes the record.
-template <int G, int MODE, bool IMPLICIT, bool LINE, class RD>
+template <int G, int MODE, bool IMPLICIT, bool LINE, bool NHC, class RD>
 __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, uint32_t acc, const RD& rd,
                                              const uint8_t* winb, uint32_t head, uint64_t a0, uint32_t len,
                                              uint64_t r, int lane, u32x4* win, uint64_t base, uint32_t* gsh) {
@@ -308,12 +315,14 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
     const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
     const uint32_t l4_off = l4 ? g.l4_off : 0u;
     uint32_t pre = 0;  // aligned-word sum contribution of the bytes [0, l4_off)
-    for (uint32_t i = lane; 2 * i < l4_off; i += G) {
-        // l4_off is even: record offset 2i is the low byte of an aligned little-endian
-        // word for an even record start, the high byte for an odd one
+    for (uint32_t i = lane; NHC ? 2 * i + 1 < l4_off : 2 * i < l4_off; i += G) {
+        // record offset 2i is the low byte of an aligned little-endian word for an even record
+        // start, the high byte for an odd one (l4_off is even on the IP path)
         const uint32_t e = rd(2 * i), o = rd(2 * i + 1);
         pre += odd ? ((e << 8) + o) : (e + (o << 8));
     }
+    // an odd l4_off (6LoWPAN NHC UDP payloads) leaves one byte, weighted by its address parity
+    if (NHC && (l4_off & 1u) && lane == 0) pre += rd(l4_off - 1) << (8u * (uint32_t)((a0 + l4_off - 1) & 1u));
     uint32_t hsum = 0, psum = 0;
     if (g.fam == 4) {
         for (uint32_t i = lane; i < g.ip_hl / 2; i += G) {
@@ -326,6 +335,11 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
             const uint32_t o = head + g.addr_off + 2 * i;
             psum += (winb[o] << 8) | winb[o + 1];
         }
+    }
+    if (NHC && l4 && g.proto == P_NHC_UDP && lane < 8) {
+        // the IPv6 addresses come with the batch (the IPHC header compresses them): 32 B per record
+        const uint32_t v = ld_u32_sync((uint64_t)p.addrs + 32ull * r + 4u * (uint32_t)lane);
+        psum = ((v & 0xffu) << 8 | ((v >> 8) & 0xffu)) + (((v >> 16) & 0xffu) << 8 | (v >> 24));
     }
     const uint32_t tot = group_sum<G>(acc);
     pre = group_sum<G>(pre);
@@ -348,7 +362,34 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
             }
         }
         uint32_t l4_valid = 1, l4_ok = 1, partial = 0;
-        if (l4) {
+        uint32_t nb0 = NO_FIELD;  // emit: new dispatch byte (NHC UDP: the C bit cleared)
+        if (NHC && l4 && g.proto == P_NHC_UDP) {
+            // 6LoWPAN NHC UDP: !combine([pseudo_header_v6(src, dst, Udp, n + 8), sport, dport,
+            // n + 8, data(payload)]) — nhc.rs:705-716 (parse), :760-771 (emit).  Ports as the
+            // accessors read them (nhc.rs:513-577, quirks included); on emit the mode-0b01
+            // destination comes from byte 3, where set_ports put it (:655-662).
+            const uint32_t b0 = rd(0), m = b0 & 3u;
+            const uint32_t sport = m <= 1 ? (rd(1) << 8 | rd(2)) : m == 2 ? 0xf000u + rd(1) : 0xf0b0u + (rd(1) >> 4);
+            uint32_t dport = m == 0 ? (rd(3) << 8 | rd(4)) : m == 1 ? 0xf000u + rd(1) : m == 2 ? (rd(2) << 8 | rd(3))
+                                                                                          : 0xf0b0u + rd(1);
+            if (EMITS && m == 1) dport = 0xf000u + rd(3);
+            const uint32_t n8 = (g.l4_len + 8) & 0xffffu;
+            const uint32_t f = fold32(tot - pre);
+            const uint32_t dat = ((a0 + g.l4_off) & 1u) ? f : bswap16(f);  // == checksum::data(payload)
+            const uint32_t ph = fold32(psum + P_UDP + n8);
+            const uint32_t chk = ~fold32(ph + sport + dport + n8 + dat) & 0xffffu;
+            if (EMITS) {
+                if (caps_tx(p.caps_udp)) {  // set_checksum, nhc.rs:676-681 (no 0 -> 0xffff)
+                    fl4 = g.fo;
+                    vl4 = chk;
+                    if (b0 & 4u) nb0 = b0 & ~4u;
+                }
+            } else {
+                const bool present = !(b0 & 4u);
+                l4_valid = present ? (chk == ((rd(g.fo) << 8) | rd(g.fo + 1))) : 1u;
+                l4_ok = caps_rx(p.caps_udp) ? l4_valid : 1u;
+            }
+        } else if (l4) {
             const uint32_t fpos = g.l4_off + g.fo;
             const uint32_t field = (rd(fpos) << 8) | rd(fpos + 1);
             // aligned-word sum of the L4 span = lanes' sum of [0, span_end) minus the
@@ -415,6 +456,7 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
             } else {
                 if (fip != MF_NONE) store_be16(wrec + fip, vip);
                 if (fl4 != MF_NONE) store_be16(wrec + fl4, vl4);
+                if (NHC && nb0 != NO_FIELD) wrec[0] = (uint8_t)nb0;
             }
             if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
         } else {
@@ -468,7 +510,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
-template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE>
+template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           uint32_t* gsh, int gib) {
@@ -493,7 +535,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     RecRef nxt2 = w.nxt;
     {
         const uint64_t r3 = r2 + ngroups < p.n ? r2 + ngroups : p.n - 1;
-        const RecRef t = rec_at<IMPLICIT, COPY>(p, r3);
+        const RecRef t = rec_at<IMPLICIT, COPY, NHC>(p, r3);
         if (last) nxt2 = t;
     }
 
@@ -546,7 +588,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                 w.g = Geom{};
                 w.g.st = SMOL_ST_MALFORMED;  // copy range does not fit: record left untouched
             } else {
-                w.g = parse_geometry(rd, w.cur.len, w.cur.kind);
+                w.g = parse_geometry<NHC>(rd, w.cur.len, w.cur.kind, MODE == MODE_EMIT);
             }
             // the lanes sum [0, span_end): the header part is subtracted at the end
             w.s1 = (w.g.proto != P_NONE && !(w.g.st & SMOL_ST_MALFORMED)) ? (int)w.g.span_end : 0;
@@ -630,7 +672,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const uint32_t tot = group_sum<G>(s_rel);
             if (lane == 0) ((gu16)p.out16)[r] = (uint16_t)bswap16(fold32(tot));
         } else {
-            finish_gates<G, MODE, IMPLICIT, LINE>(p, w.g, w.acc, rd, winb, head, w.cur.a0, w.cur.len, r, lane, win,
+            finish_gates<G, MODE, IMPLICIT, LINE, NHC>(p, w.g, w.acc, rd, winb, head, w.cur.a0, w.cur.len, r, lane, win,
                                                   base, gsh);
         }
     }
@@ -647,7 +689,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 
 // MODE_DATA: checksum::data over [0, len).  MODE_EMIT / MODE_VERIFY: the protocol gates.
 // MODE_COPY: payload copy + emit in one pass.  VAR: see VarT.
-template <int G, int U, int MODE, bool IMPLICIT, int VAR>
+template <int G, int U, int MODE, bool IMPLICIT, int VAR, bool NHC = false>
 __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool NT = VarT<VAR>::NT;
     constexpr bool PF = VarT<VAR>::PF;
@@ -669,8 +711,8 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     Walk w;
     w.r = (uint64_t)blockIdx.x * GPB + gib;
     if (w.r >= p.n) return;
-    w.cur = rec_at<IMPLICIT, COPY>(p, w.r);
-    w.nxt = rec_at<IMPLICIT, COPY>(p, w.r + ngroups < p.n ? w.r + ngroups : p.n - 1);
+    w.cur = rec_at<IMPLICIT, COPY, NHC>(p, w.r);
+    w.nxt = rec_at<IMPLICIT, COPY, NHC>(p, w.r + ngroups < p.n ? w.r + ngroups : p.n - 1);
     w.nch = n_chunks<LINE>(w.cur);
     w.step = 0;
     w.g = Geom{};
@@ -685,14 +727,14 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
                                         shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, va, vb, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, vb, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC>(p, w, va, vb, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC>(p, w, vb, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
         }
     } else {
         while (true) {
             load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
                                             shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE>(p, w, va, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC>(p, w, va, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
         }
     }
 }
@@ -747,12 +789,12 @@ __global__ __launch_bounds__(256) void scatter_kernel(KParams p) {
 // Launch table
 // ---------------------------------------------------------------------------------------------
 
-template <int G, int U, int MODE, bool IMPLICIT, int VAR>
+template <int G, int U, int MODE, bool IMPLICIT, int VAR, bool NHC = false>
 hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    hipLaunchKernelGGL((csum_kernel<G, U, MODE, IMPLICIT, VAR>), dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((csum_kernel<G, U, MODE, IMPLICIT, VAR, NHC>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -780,6 +822,22 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
         default: return launch_shape<MODE, IMPLICIT, 0>(shape, p, max_blocks, s);
     }
+}
+
+// 6LoWPAN NHC UDP batches: the walk kernel instantiated with the NHC gates, on the two default
+// variants (1: 16-B grid, cached loads; 5: line grid, nt loads) and three shapes (other shapes map
+// to the one with the same group size or the nearest).
+template <int MODE, bool IMPLICIT>
+hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
+    if (var == 5 || var == 6) {
+        if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
+        if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
+        return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
+    }
+    if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 1, true>(p, max_blocks, s);
+    if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 1, true>(p, max_blocks, s);
+    return launch_one<16, 3, MODE, IMPLICIT, 1, true>(p, max_blocks, s);
 }
 
 // MODE_COPY keeps three chunks per lane and step (record + two source chunks), so it is built for

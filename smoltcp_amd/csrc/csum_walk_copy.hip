@@ -14,6 +14,15 @@ hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s) 
 
 hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const bool implicit = p.desc == nullptr;
+    if (p.addrs) {  // 6LoWPAN NHC UDP
+        if (mode == MODE_EMIT)
+            return implicit ? launch_walk_nhc<MODE_EMIT, true>(shape, var, p, max_blocks, s)
+                            : launch_walk_nhc<MODE_EMIT, false>(shape, var, p, max_blocks, s);
+        if (mode == MODE_VERIFY)
+            return implicit ? launch_walk_nhc<MODE_VERIFY, true>(shape, var, p, max_blocks, s)
+                            : launch_walk_nhc<MODE_VERIFY, false>(shape, var, p, max_blocks, s);
+        return hipErrorInvalidValue;
+    }
     switch (mode) {
         case MODE_DATA:
             return implicit ? launch_walk<MODE_DATA, true>(shape, var, p, max_blocks, s)

@@ -174,6 +174,33 @@ class ChecksumEngine:
                                               self._stream(stream)), "smol_csum_batch_copy_emit")
         return status
 
+    def nhc_udp_emit(self, buf, batch: Batch, addrs, caps=None, status=None, stream=None):
+        """6LoWPAN NHC UDP emit (smol_csum_batch_nhc_udp_emit): ``addrs`` is a device uint8 tensor of
+        n x 32 bytes (IPv6 source, destination per record)."""
+        self._check_buf(buf, batch)
+        assert addrs.is_cuda and addrs.numel() >= 32 * batch.n
+        b = batch.c()
+        c = _caps(caps)
+        check(lib().smol_csum_batch_nhc_udp_emit(self._h, buf.data_ptr(), ctypes.byref(b), addrs.data_ptr(),
+                                                 ctypes.byref(c), status.data_ptr() if status is not None else None,
+                                                 self._stream(stream)), "smol_csum_batch_nhc_udp_emit")
+        return status
+
+    def nhc_udp_verify(self, buf, batch: Batch, addrs, caps=None, status=None, stream=None):
+        """6LoWPAN NHC UDP parse gate (smol_csum_batch_nhc_udp_verify); returns the status tensor."""
+        import torch
+
+        self._check_buf(buf, batch)
+        assert addrs.is_cuda and addrs.numel() >= 32 * batch.n
+        if status is None:
+            status = torch.empty(batch.n, dtype=torch.uint8, device=buf.device)
+        b = batch.c()
+        c = _caps(caps)
+        check(lib().smol_csum_batch_nhc_udp_verify(self._h, buf.data_ptr(), ctypes.byref(b), addrs.data_ptr(),
+                                                   ctypes.byref(c), status.data_ptr(), self._stream(stream)),
+              "smol_csum_batch_nhc_udp_verify")
+        return status
+
     def verify(self, buf, batch: Batch, caps=None, status=None, stream=None):
         """status[i] = SMOL_ST_* bits (Repr::parse gates under ``caps``)."""
         import torch

@@ -191,6 +191,25 @@ public:
         check(smol_csum_batch_verify(ctx_, d_buf, &bc, &cc, d_status, stream), "smol_csum_batch_verify");
     }
 
+    // 6LoWPAN NHC UDP (sixlowpan::nhc::UdpNhcRepr::emit / ::parse): every record is a LOWPAN_NHC
+    // UDP packet; d_addrs[i] holds record i's IPv6 addresses (IPHC-decompressed).
+    void nhc_udp_emit(uint8_t* d_buf, const Batch& b, const smol_ipv6_addr_pair_t* d_addrs,
+                      const smoltcp::phy::ChecksumCapabilities& caps = {}, uint8_t* d_status = nullptr,
+                      void* stream = nullptr) {
+        auto bc = b.c();
+        auto cc = caps.c();
+        check(smol_csum_batch_nhc_udp_emit(ctx_, d_buf, &bc, d_addrs, &cc, d_status, stream),
+              "smol_csum_batch_nhc_udp_emit");
+    }
+    void nhc_udp_verify(const uint8_t* d_buf, const Batch& b, const smol_ipv6_addr_pair_t* d_addrs,
+                        uint8_t* d_status, const smoltcp::phy::ChecksumCapabilities& caps = {},
+                        void* stream = nullptr) {
+        auto bc = b.c();
+        auto cc = caps.c();
+        check(smol_csum_batch_nhc_udp_verify(ctx_, d_buf, &bc, d_addrs, &cc, d_status, stream),
+              "smol_csum_batch_nhc_udp_verify");
+    }
+
     // checksum::data over every record span.
     void data(const uint8_t* d_buf, const Batch& b, uint16_t* d_out, void* stream = nullptr) {
         auto bc = b.c();

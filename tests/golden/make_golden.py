@@ -65,6 +65,54 @@ FF02_1 = "ff020000000000000000000000000001"  # IPV6_LINK_LOCAL_ALL_NODES (mld.rs
 FF02_2 = "ff020000000000000000000000000002"  # IPV6_LINK_LOCAL_ALL_ROUTERS
 
 
+def _eui64_iid(ext_le: bytes) -> bytes:
+    """IPv6 interface identifier of an IEEE 802.15.4 extended address as it sits in the frame
+    (little-endian): reverse the bytes, flip the universal/local bit (RFC 4944 §6)."""
+    ext = ext_le[::-1]
+    return bytes([ext[0] ^ 0x02]) + ext[1:]
+
+
+def sixlowpan_nhc_udp():
+    """The 6LoWPAN NHC UDP datagram of test sixlowpan_three_fragments (src/wire/sixlowpan/mod.rs):
+    three IEEE 802.15.4 frames (2003 frame, PAN-ID compression, extended addresses: 21-byte MAC
+    header), FRAG1 (4 bytes) + IPHC 0x6e33 (TF=01: 3 bytes inline, NH compressed, HLIM elided,
+    SAM=DAM=11: addresses from the link-layer addresses) + NHC UDP, then two FRAGN (5 bytes).  The
+    reassembled NHC UDP packet and its link-local addresses; its inline checksum 0xb46b is what
+    UdpNhcRepr::parse (nhc.rs:697-723) checks under caps.udp.rx().  (The datagram of
+    src/iface/interface/tests/sixlowpan.rs test_sixlowpan_udp_with_fragmentation is not used: that
+    test disables UDP checksums and its inline checksum does not match its payload.)"""
+    rel = "src/wire/sixlowpan/mod.rs"
+    text = _read(rel)
+    frames, lines = [], []
+    for name in ("frame1", "frame2", "frame3"):
+        m = re.search(r"let %s: &\[u8\] = &\[(.*?)\];" % name, text, re.S)
+        if not m:
+            raise SystemExit(f"{rel}: {name} not found")
+        frames.append(_parse_array(m.group(1)))
+        lines.append(text[: m.start()].count("\n") + 1)
+    mac = 21
+    f1, f2, f3 = frames
+    assert f1[mac] >> 3 == 0x18 and f2[mac] >> 3 == 0x1C and f3[mac] >> 3 == 0x1C  # FRAG1 / FRAGN
+    iphc = f1[mac + 4:]
+    assert iphc[0] == 0x6E and iphc[1] == 0x33
+    nhc = iphc[2 + 3:]  # TF=01 carries 3 bytes
+    assert nhc[0] >> 3 == 0x1E and nhc[0] & 7 == 0  # UDP, checksum inline, both ports inline
+    pkt = nhc + f2[mac + 5:] + f3[mac + 5:]
+    size = (f1[mac] & 7) << 8 | f1[mac + 1]  # datagram_size (uncompressed IPv6 + UDP + payload)
+    assert len(pkt) - 7 == size - 48
+    dst_le, src_le = f1[5:13], f1[13:21]
+    return [{
+        "name": "sixlowpan_three_fragments_udp",
+        "bytes": pkt.hex(),
+        "src": (bytes.fromhex("fe80000000000000") + _eui64_iid(src_le)).hex(),
+        "dst": (bytes.fromhex("fe80000000000000") + _eui64_iid(dst_le)).hex(),
+        "src_port": nhc[1] << 8 | nhc[2], "dst_port": nhc[3] << 8 | nhc[4],
+        "checksum": nhc[5] << 8 | nhc[6], "verify": True,
+        "cite": f"{rel}:{lines[0]},{lines[1]},{lines[2]} sixlowpan_three_fragments (datagram_size 307, "
+                "tag 0x3f), reassembled",
+    }]
+
+
 def main():
     kats = []
 
@@ -135,16 +183,20 @@ def main():
             corpus.append({"name": fn, "kind": "eth", "bytes": f.read().hex(),
                            "cite": f"fuzz/corpus/packet_parser/{fn} (0BSD)"})
 
+    nhc = sixlowpan_nhc_udp()
+
     doc = {
         "generator": "tests/golden/make_golden.py",
         "reference": "smoltcp 0.13.1 (/root/reference, Cargo.toml:3)",
         "kat": kats,
         "iface_ipv6_packets": packets,
         "fuzz_corpus_frames": corpus,
+        "sixlowpan_nhc_udp": nhc,
     }
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)
-    print(f"wrote {OUT}: {len(kats)} KATs, {len(packets)} iface IPv6 packets, {len(corpus)} frames")
+    print(f"wrote {OUT}: {len(kats)} KATs, {len(packets)} iface IPv6 packets, {len(corpus)} frames, "
+          f"{len(nhc)} 6LoWPAN NHC UDP packets")
 
 
 if __name__ == "__main__":

@@ -63,6 +63,16 @@ def rand_bytes(rng, n: int) -> bytes:
     return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
 
 
+NHC_PORTS_SIZE = {0: 4, 1: 3, 2: 3, 3: 1}  # UdpNhcPacket::ports_size, nhc.rs:602-611
+
+
+def nhc_udp(rng, mode: int, elided: bool, plen: int, csum: int = 0) -> bytes:
+    """A LOWPAN_NHC UDP packet (RFC 6282 §4.3): dispatch 0b11110CPP, ports in mode ``mode``
+    (random inline bytes), an inline checksum unless ``elided``, ``plen`` random payload bytes."""
+    head = bytes([0xF0 | (4 if elided else 0) | mode]) + rand_bytes(rng, NHC_PORTS_SIZE[mode])
+    return head + (b"" if elided else be16(csum)) + rand_bytes(rng, plen)
+
+
 def pack(records, align: int = 1, gap_rng=None, base_pad: int = 0):
     """Pack byte records into one host buffer; returns (buf, offsets, lengths).  ``gap_rng`` adds
     random 0..7 byte gaps (odd offsets)."""
