@@ -47,10 +47,6 @@
 
 namespace smolcsum {
 
-#ifndef SMOL_SKIPD
-#define SMOL_SKIPD 1  // experiments build a copy with -DSMOL_SKIPD=0
-#endif
-
 // Kernel variants: load cache policy, register prefetch, chunk-grid alignment.
 // 0 = nt + prefetch, 1 = plain + prefetch, 2 = nt without prefetch (16-byte grid);
 // 5 = nt + prefetch, 6 = plain + prefetch (128-byte line grid).  3 / 4 are the tile kernel.
@@ -472,13 +468,7 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
         if (p.patch && p.lines) {  // copy the patched line(s) from the window to the slot
             wave_lds_sync();
             const uint32_t lines = *gsh;
-#if defined(SMOL_EXP_NOSLOT)
-            const uint32_t nc = 0, c0 = lines & 0xffu;  // experiment: no slot copies
-#elif defined(SMOL_EXP_SLOT64)
-            const uint32_t nc = lines ? 4u : 0u, c0 = lines & 0xffu;  // experiment: one line only
-#else
             const uint32_t nc = 4u * (lines >> 8), c0 = lines & 0xffu;
-#endif
             for (uint32_t c = (uint32_t)lane; c < nc; c += G)
                 *(GMEM u32x4*)((uint64_t)p.lines + (uint64_t)LINE_SLOT * r + 16u * c) = win[c0 + c];
         }
@@ -698,7 +688,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     // a natural grid), measured 1-1.5 % faster (C2 verify 0.2444 -> 0.2422 ms, C4 0.2219 -> 0.2189
     // ms).  Descriptor batches keep the unconditional prefetch: there the conditional load made
     // C3 verify 25 % slower (0.810 -> 0.989 ms).
-    constexpr bool SKIPD = SMOL_SKIPD && IMPLICIT;
+    constexpr bool SKIPD = IMPLICIT;
     constexpr bool COPY = MODE == MODE_COPY;
     constexpr int GPB = 256 / G;
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");

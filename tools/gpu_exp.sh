@@ -13,12 +13,11 @@ step() {  # step <name> <seconds> <cmd...>: stop on the first failure
     if [ $rc -ne 0 ]; then tail -30 "$O/$name.log"; exit $rc; fi
     tail -${TAILN:-1} "$O/$name.log"
 }
-TAILN=3 step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-for lib in default NOSHARE; do
+for lib in default w5 w6; do
 L=smoltcp_amd/libsmolcsum.so; [ $lib != default ] && L=build_alt/lib_$lib.so
-for c in c2 c4; do
-    SMOLCSUM_LIB=$L TAILN=0 step sweep_${c}_$lib 600 python tools/sweep.py --config $c --shapes 0,7 --var 1,5 --defer 0
-    grep '"round": 1' $O/sweep_${c}_$lib.log | cut -c1-140
+for c in c2 c4 c3; do
+    SMOLCSUM_LIB=$L step bench_${c}_$lib 300 python bench.py --config $c --cpu-seconds 0
+    python3 -c "import json,sys; d=json.loads(open('$O/bench_${c}_$lib.log').read().strip().splitlines()[-1]); print('   ', '$lib', '$c', d['value'], d['unit'], d['kernels_ms'])"
 done
 done
 echo "== done"
