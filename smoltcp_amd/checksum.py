@@ -43,6 +43,26 @@ def pseudo_header_v6(src_addr: bytes, dst_addr: bytes, next_header: int, length:
                                                 length & 0xFFFFFFFF))
 
 
+def format_checksum(correct: bool, partially_correct: bool) -> str:
+    """checksum::format_checksum (src/wire/ip.rs:871-886): the annotation the pretty-printers
+    append to a packet line."""
+    if correct:
+        return ""
+    return " (partial checksum correct)" if partially_correct else " (checksum incorrect)"
+
+
+def ipv4_annotation(status: int) -> str:
+    """The IPv4 header line's annotation for a verify status byte (Ipv4Packet's pretty_print,
+    src/wire/ipv4.rs:698: format_checksum(verify_checksum(), false))."""
+    return format_checksum(bool(status & 0x08), False)  # SMOL_ST_IP_VALID
+
+
+def l4_annotation(status: int) -> str:
+    """The UDP / TCP line's annotation (pretty_print_ip_payload, src/wire/ip.rs:930-962:
+    verify_checksum() and verify_partial_checksum())."""
+    return format_checksum(bool(status & 0x10), bool(status & 0x04))  # L4_VALID, L4_PARTIAL
+
+
 def pseudo_header(src_addr: bytes, dst_addr: bytes, next_header: int, length: int) -> int:
     """checksum::pseudo_header (src/wire/ip.rs:851-869): dispatch on the address family."""
     fam = {4: 4, 16: 6}

@@ -82,6 +82,21 @@ inline uint16_t pseudo_header(std::span<const uint8_t> src, std::span<const uint
     return out;
 }
 
+// checksum::format_checksum (ip.rs:871-886): the annotation the packet pretty-printers append.
+inline const char* format_checksum(bool correct, bool partially_correct) {
+    if (correct) return "";
+    return partially_correct ? " (partial checksum correct)" : " (checksum incorrect)";
+}
+
+// The annotations of one verify status byte (SMOL_ST_*): the IPv4 header line
+// (Ipv4Packet pretty_print, ipv4.rs:698: format_checksum(verify_checksum(), false)) and the
+// UDP / TCP line (pretty_print_ip_payload, ip.rs:930-962: verify_checksum() and
+// verify_partial_checksum()).
+inline const char* ipv4_annotation(uint8_t status) { return format_checksum(status & SMOL_ST_IP_VALID, false); }
+inline const char* l4_annotation(uint8_t status) {
+    return format_checksum(status & SMOL_ST_L4_VALID, status & SMOL_ST_L4_PARTIAL);
+}
+
 }  // namespace wire::checksum
 
 // ---- phy::Checksum / phy::ChecksumCapabilities (src/phy/mod.rs:173-234) -------------------------

@@ -113,6 +113,22 @@ def sixlowpan_nhc_udp():
     }]
 
 
+def pretty_print_example():
+    """The frame of the module example of src/wire/pretty_print.rs and the IPv4 line's checksum
+    annotation its expected listing shows (format_checksum, src/wire/ip.rs:871-886)."""
+    rel = "src/wire/pretty_print.rs"
+    text = _read(rel)
+    m = re.search(r"let buffer = vec!\[(.*?)\];", text, re.S)
+    body = re.sub(r"//[^\n]*", "", m.group(1))
+    frame = _parse_array(body)
+    lines = re.findall(r"IPv4 src=.*?proto=\w+( \([^)]*\))?\\n", text)
+    return [{
+        "name": "pretty_print_module_example", "kind": "eth", "bytes": frame.hex(),
+        "ipv4_annotation": lines[0] if lines else "",
+        "cite": f"{rel}:{text[: m.start()].count(chr(10)) + 1} (module doc example)",
+    }]
+
+
 def main():
     kats = []
 
@@ -184,6 +200,7 @@ def main():
                            "cite": f"fuzz/corpus/packet_parser/{fn} (0BSD)"})
 
     nhc = sixlowpan_nhc_udp()
+    pretty = pretty_print_example()
 
     doc = {
         "generator": "tests/golden/make_golden.py",
@@ -192,6 +209,7 @@ def main():
         "iface_ipv6_packets": packets,
         "fuzz_corpus_frames": corpus,
         "sixlowpan_nhc_udp": nhc,
+        "pretty_print": pretty,
     }
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)

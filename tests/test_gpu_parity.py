@@ -576,3 +576,20 @@ def test_variants_fixed_stride(eng, variant):
                     assert np.array_equal(st, ref_v), (variant, L, stride, shape, blocks)
                     assert np.array_equal(got, ref_e), (variant, L, stride, shape, blocks)
                     assert np.array_equal(est.cpu().numpy(), ref_es)
+
+
+def test_pretty_print_annotations(eng, golden):
+    """The pretty-print path's checksum annotations (checksum::format_checksum, src/wire/ip.rs:
+    871-886) from the DEVICE verify status: the module example of src/wire/pretty_print.rs reads
+    "(checksum incorrect)" on its IPv4 line, the corpus frames with TX-offload partial checksums
+    "(partial checksum correct)" on their TCP line."""
+    from smoltcp_amd import checksum
+
+    ex = golden["pretty_print"][0]
+    recs = [bytes.fromhex(ex["bytes"])] + [bytes.fromhex(f["bytes"]) for f in golden["fuzz_corpus_frames"]]
+    st, _, _, _ = _run_records(eng, recs, E.KIND_ETH, gap_seed=5)
+    assert checksum.ipv4_annotation(int(st[0])) == ex["ipv4_annotation"] == " (checksum incorrect)"
+    partial = {"tcpv4_data.bin", "tcpv4_fin.bin", "tcpv4_syn.bin"}
+    for f, s in zip(golden["fuzz_corpus_frames"], st[1:]):
+        want = " (partial checksum correct)" if f["name"] in partial else ""
+        assert checksum.l4_annotation(int(s)) == want, f["name"]
