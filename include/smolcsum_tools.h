@@ -44,7 +44,8 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
  * step, 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch; or at its
  * 128-byte line boundary: 5 = non-temporal loads + prefetch, 6 = plain loads + prefetch.
  * 3 / 4 = the "tile" kernel (groups only stream and sum, lanes finish 64 records at once) with
- * non-temporal / plain loads — emit and verify only (data() uses the walk kernel). */
+ * non-temporal / plain loads on the 16-byte grid, 7 = the tile kernel with non-temporal loads on
+ * the line grid — emit and verify only (data() uses the walk kernel). */
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
 
 /* Tile kernel: records per wavefront tile, 32 (default) or 64. */

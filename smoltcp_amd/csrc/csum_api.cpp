@@ -174,9 +174,10 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     // grid), 3-4 = tile kernel (csum_tile.hip: nt / plain loads), emit and verify only.
     int variant = ctx->variant;
     if (variant < 0) variant = auto_variant(mode, b->desc != nullptr);
-    if (mode == MODE_DATA && (variant == 3 || variant == 4)) variant = 0;
-    if (d_addrs && (variant == 3 || variant == 4)) variant = auto_variant(mode, b->desc != nullptr);  // walk only
-    const bool use_tile = variant == 3 || variant == 4;
+    const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
+    if (mode == MODE_DATA && tile_var) variant = 0;
+    if (d_addrs && tile_var) variant = auto_variant(mode, b->desc != nullptr);  // walk only
+    const bool use_tile = variant == 3 || variant == 4 || variant == 7;
     int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr, line_grid(variant));
     // Two-pass emit only on request: it trades the in-pass 2-byte stores for a meta word + line
     // slot per record and a scatter pass, and measured slower (C2: read pass 0.301 ms + scatter
@@ -189,7 +190,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         return SMOL_OK;
     }
     if (use_tile && !(mode == MODE_EMIT && two_pass)) {
-        hipError_t e = launch_tile(mode, shape, variant - 3, ctx->tile_records, p, ctx->max_blocks, s);
+        hipError_t e = launch_tile(mode, shape, variant == 7 ? 2 : variant - 3, ctx->tile_records, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         return SMOL_OK;
     }
@@ -440,7 +441,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 6) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 7) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

@@ -52,7 +52,7 @@ struct WaveLds {
 
 struct Slot {
     uint64_t a0;
-    uint32_t len, nch;
+    uint32_t len, nch;  // nch: chunks of the load grid
 };
 
 __device__ __forceinline__ uint32_t ld_byte_sync(uint64_t a) {
@@ -117,10 +117,13 @@ __device__ __forceinline__ uint32_t region_sum(const uint32_t* row, uint64_t bas
     return acc;
 }
 
-// VAR: 0 = non-temporal record loads (default), 1 = plain loads.
+// VAR: 0 = non-temporal record loads, 1 = plain loads (both on the record's 16-byte grid),
+// 2 = non-temporal loads on the record's 128-byte line grid (see csum_walk.h: nt loads need whole
+// lines; the chunks before the record are loaded and not summed).
 template <int G, int U, int MODE, bool IMPLICIT, int VAR, int TILE>
 __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
     constexpr bool NT = VAR != 1;
+    constexpr uint64_t GRID = VAR == 2 ? 128 : 16;  // load-grid alignment
     constexpr int GPW = 64 / G;  // groups per wavefront
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     static_assert(TILE == 32 || TILE == 64, "tile");
@@ -175,11 +178,11 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
                 sl.a0 = (uint64_t)L.info[3 * q] | ((uint64_t)L.info[3 * q + 1] << 32);
                 sl.len = L.info[3 * q + 2];
             }
-            sl.nch = sl.len ? (uint32_t)(((sl.a0 + sl.len + 15) >> 4) - (sl.a0 >> 4)) : 0u;
+            sl.nch = sl.len ? (uint32_t)(((sl.a0 + sl.len + 15) >> 4) - ((sl.a0 & ~(GRID - 1)) >> 4)) : 0u;
             return sl;
         };
         auto load = [&](u32x4 (&v)[U], const Slot& sl, uint32_t step, bool valid) {
-            const uint64_t base = sl.a0 & ~15ull;
+            const uint64_t base = sl.a0 & ~(GRID - 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t k = step * (G * U) + u * G + gl;
@@ -202,14 +205,23 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
         uint32_t acc = 0;
         auto process = [&](const u32x4 (&v)[U], const Slot& sl, int j, uint32_t step) {
             const int q = j * GPW + grp;
-            if (step == 0 && gl < WIN / 16 && (uint32_t)gl < sl.nch) {
-                uint32_t* row = &L.win[q * WSTRIDE + 4 * gl];
-                row[0] = v[0].x;
-                row[1] = v[0].y;
-                row[2] = v[0].z;
-                row[3] = v[0].w;
+            // the window holds the chunks from the record's 16-byte boundary: grid chunks k0 ..
+            const uint32_t k0 = (uint32_t)((sl.a0 & (GRID - 1)) >> 4);
+            if (step == 0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t k = (uint32_t)(u * G + gl);
+                    if (GRID == 16 && u > 0) break;
+                    if (k >= k0 && k - k0 < (uint32_t)(WIN / 16) && k < sl.nch) {
+                        uint32_t* row = &L.win[q * WSTRIDE + 4 * (k - k0)];
+                        row[0] = v[u].x;
+                        row[1] = v[u].y;
+                        row[2] = v[u].z;
+                        row[3] = v[u].w;
+                    }
+                }
             }
-            const int endrel = (int)((uint32_t)(sl.a0 & 15u) + sl.len);  // record end, from base
+            const int endrel = (int)((uint32_t)(sl.a0 & (GRID - 1)) + sl.len);  // record end, from the grid
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t k = step * (G * U) + u * G + gl;
@@ -221,6 +233,7 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
                     c.z = mask_dword(c.z, 0, lim - 8);
                     c.w = mask_dword(c.w, 0, lim - 12);
                 }
+                if (GRID > 16 && k < k0) c = u32x4{0u, 0u, 0u, 0u};  // wholly before the record
                 acc = add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, acc))));
             }
             const uint32_t nst = sl.nch ? (sl.nch + (G * U) - 1) / (G * U) : 1u;
@@ -372,8 +385,10 @@ static hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t 
 template <int MODE, bool IMPLICIT, int VAR, int TILE>
 static hipError_t launch_shape(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (shape) {
-        case CFG_G8U6: return launch_one<8, 6, MODE, IMPLICIT, VAR, TILE>(p, max_blocks, s);
-        case CFG_G16U3: return launch_one<16, 3, MODE, IMPLICIT, VAR, TILE>(p, max_blocks, s);
+        case CFG_G8U6:
+        case CFG_G8U7: return launch_one<8, 6, MODE, IMPLICIT, VAR, TILE>(p, max_blocks, s);
+        case CFG_G16U3:
+        case CFG_G16U4: return launch_one<16, 3, MODE, IMPLICIT, VAR, TILE>(p, max_blocks, s);
         case CFG_G16U6: return launch_one<16, 6, MODE, IMPLICIT, VAR, TILE>(p, max_blocks, s);
         case CFG_G32U3: return launch_one<32, 3, MODE, IMPLICIT, VAR, TILE>(p, max_blocks, s);
         case CFG_G32U4: return launch_one<32, 4, MODE, IMPLICIT, VAR, TILE>(p, max_blocks, s);
@@ -388,6 +403,10 @@ static hipError_t launch_mode(int shape, int var, const KParams& p, uint32_t max
     if (var == 1) {
         return implicit ? launch_shape<MODE, true, 1, TILE>(shape, p, max_blocks, s)
                         : launch_shape<MODE, false, 1, TILE>(shape, p, max_blocks, s);
+    }
+    if (var == 2) {
+        return implicit ? launch_shape<MODE, true, 2, TILE>(shape, p, max_blocks, s)
+                        : launch_shape<MODE, false, 2, TILE>(shape, p, max_blocks, s);
     }
     return implicit ? launch_shape<MODE, true, 0, TILE>(shape, p, max_blocks, s)
                     : launch_shape<MODE, false, 0, TILE>(shape, p, max_blocks, s);

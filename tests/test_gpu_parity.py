@@ -539,7 +539,7 @@ def test_emit_two_pass_chunks(eng):
         _emit_case(eng, host, off, n, stride, L, E.KIND_IP, CAPS_DEFAULT, -1, None)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_variants_fixed_stride(eng, variant):
     """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
     the oracle on fixed-stride batches: strides equal to the record length (neighbours share

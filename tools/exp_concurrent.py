@@ -43,17 +43,19 @@ def main():
         eng.verify(wl.rx, wl.batch, status=wl.status, stream=s0)
         eng.emit(wl.tx, wl.batch, stream=s0)
 
-    def timeit(name, fn):
-        for _ in range(5):
-            fn()
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s0)
-        for _ in range(reps):
-            fn()
-        b.record(s0)
-        torch.cuda.synchronize()
-        ms = a.elapsed_time(b) / reps
+    def timeit(name, fn, steps_per_call=1):
+        # everything (including graph replays, which launch on the current stream) runs on s0
+        with torch.cuda.stream(s0):
+            for _ in range(5):
+                fn()
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s0)
+            for _ in range(reps):
+                fn()
+            b.record(s0)
+            torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / reps / steps_per_call
         gib = 2 * wl.span_bytes / (ms * 1e-3) / 2**30
         print(json.dumps({"cfg": cfg, "case": name, "ms_per_step": round(ms, 4), "GiB/s": round(gib, 1)}), flush=True)
 
@@ -65,14 +67,12 @@ def main():
         with torch.cuda.graph(g, stream=s0):
             for _ in range(10):
                 serial()
-        timeit("graph of 10 serial steps (per step)", lambda: g.replay())
+        timeit("graph of 10 serial steps (per step)", lambda: g.replay(), 10)
         g2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g2, stream=s0):
             for _ in range(10):
                 forked()
-        timeit("graph of 10 forked steps (per step)", lambda: g2.replay())
-    # the graph timings above are per replay of 10 steps: report per step
-    print("note: graph cases time 10 steps per replay", flush=True)
+        timeit("graph of 10 forked steps (per step)", lambda: g2.replay(), 10)
 
 
 if __name__ == "__main__":
