@@ -341,7 +341,8 @@ def main():
         dom = max(kernels, key=lambda k: kernels[k]["ms"])
         kd = kernels[dom]
         achieved = kd["bytes"] / (kd["ms"] * 1e-3) / 1e9
-        traffic, tsrc = load_traffic(args.config, "copy_emit" if (wl.copy is not None and dom == "emit") else dom)
+        dop = "copy_emit" if (wl.copy is not None and dom == "emit") else dom
+        traffic, tsrc = load_traffic(args.config, dop)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -357,7 +358,7 @@ def main():
             "data": "synthetic: device-generated packets (splitmix64 payload, seeded), HBM-resident",
             "config": {"workload": wl.workload, "records_per_gpu": wl.n, "parallelism": f"shard x{world} (no collective)",
                        "checksummed_bytes_per_step_per_gpu": 2 * wl.span_bytes},
-            "roofline": {"bound": "hbm", "kernel": f"csum_kernel ({'copy_emit' if (wl.copy is not None and dom == 'emit') else dom})", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": f"{eng.kernel_name(dop, wl.desc_bytes > 0)} ({dop})", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": tsrc,
                          "algorithmic_bytes_per_launch": kd["bytes"], "launch_ms": round(kd["ms"], 4)},

@@ -69,6 +69,10 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
 /* The launch shape the library picks for a verify over an implicit batch of `len`-byte records. */
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc);
 
+/* The kernel (the rocprofv3 name prefix: "csum_kernel" or "csum_tile_kernel") that an IP-path
+ * operation runs with this context's variant setting: op 0 data, 1 emit, 2 verify, 3 copy-emit. */
+const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int has_desc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,6 +35,7 @@ TOOL_SYMBOLS = [
     "smol_csum_tool_set_variant", "smol_csum_tool_set_deferred_emit",
     "smol_csum_tool_set_tile",
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
+    "smol_csum_tool_kernel_name",
 ]
 
 
@@ -136,6 +137,8 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_tool_stream_read.restype = i32
     L.smol_csum_tool_auto_shape.argtypes = [u32, i32]
     L.smol_csum_tool_auto_shape.restype = i32
+    L.smol_csum_tool_kernel_name.argtypes = [vp, i32, i32]
+    L.smol_csum_tool_kernel_name.restype = ctypes.c_char_p
     _LIB = L
     return L
 

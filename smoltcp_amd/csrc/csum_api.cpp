@@ -88,9 +88,13 @@ constexpr uint32_t kNaturalGrid = 0x7fffffffu;
 // Kernel variant when none is forced (tools/sweep.py on MI355X, C2 / C3 / C4): the 128-byte line
 // grid with non-temporal loads (verify: C2 0.2415 -> 0.2327 ms, C4 0.2158 -> 0.2083 ms, C3 0.826 ->
 // 0.815 ms; fixed-stride emit with shared boundary lines, csum_walk.h shared_from: C2 0.3155 ->
-// 0.304 ms, C4 0.2727 -> 0.263 ms), except emit over descriptor batches: cached loads on the
-// 16-byte grid (C3 0.9705 ms vs 0.9722 ms).
-int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 1 : 5; }
+// 0.304 ms, C4 0.2727 -> 0.263 ms), except emit over descriptor batches: the tile kernel on the
+// line grid (variant 7, C3 0.9285 ms vs the walk kernel's best 0.9945 ms at the same shape; its
+// verify is slower, 1.08 ms vs 0.83 ms).  walk_variant is the walk kernel's own choice, for the
+// entry points the tile kernel does not serve (NHC, data, copy-emit): cached loads on the 16-byte
+// grid for emit over descriptors (C3 0.9705 ms vs 0.9722 ms), the line grid otherwise.
+int walk_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 1 : 5; }
+int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : 5; }
 
 bool line_grid(int variant) { return variant == 5 || variant == 6; }
 
@@ -171,14 +175,15 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
     // Variants: 0-2, 5-6 = walk kernel (csum_walk.h VarT: load policy, prefetch, chunk
-    // grid), 3-4 = tile kernel (csum_tile.hip: nt / plain loads), emit and verify only.
+    // grid), 3-4, 7 = tile kernel (csum_tile.hip: nt / plain loads, nt on the line grid), IP emit
+    // and verify only.
     int variant = ctx->variant;
-    if (variant < 0) variant = auto_variant(mode, b->desc != nullptr);
+    const bool has_desc = b->desc != nullptr;
+    if (variant < 0) variant = auto_variant(mode, has_desc);
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
-    if (mode == MODE_DATA && tile_var) variant = 0;
-    if (d_addrs && tile_var) variant = auto_variant(mode, b->desc != nullptr);  // walk only
+    if (tile_var && (mode == MODE_DATA || mode == MODE_COPY || d_addrs)) variant = walk_variant(mode, has_desc);
     const bool use_tile = variant == 3 || variant == 4 || variant == 7;
-    int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, b->desc != nullptr, line_grid(variant));
+    int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, has_desc, line_grid(variant));
     // Two-pass emit only on request: it trades the in-pass 2-byte stores for a meta word + line
     // slot per record and a scatter pass, and measured slower (C2: read pass 0.301 ms + scatter
     // 0.047 ms against 0.315 ms in one pass; the slot writes alone cost 0.049 ms).
@@ -477,6 +482,14 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
 
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
     return auto_shape(len, has_desc != 0, line_grid(auto_variant(MODE_VERIFY, has_desc != 0)));
+}
+
+const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int has_desc) {
+    if (!ctx || op < MODE_DATA || op > MODE_COPY) return "";
+    const int v = ctx->variant >= 0 ? ctx->variant : auto_variant(op, has_desc != 0);
+    const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY) &&
+                      !(op == MODE_EMIT && ctx->defer_emit == 1);
+    return tile ? "csum_tile_kernel" : "csum_kernel";
 }
 
 }  // extern "C"

@@ -253,6 +253,11 @@ class ChecksumEngine:
     def set_tile(self, records: int):
         check(lib().smol_csum_tool_set_tile(self._h, int(records)), "smol_csum_tool_set_tile")
 
+    def kernel_name(self, op: str, has_desc: bool = False) -> str:
+        """The kernel an IP-path `op` ("data", "emit", "verify", "copy_emit") launches here."""
+        code = {"data": 0, "emit": 1, "verify": 2, "copy_emit": 3}[op]
+        return lib().smol_csum_tool_kernel_name(self._h, code, int(bool(has_desc))).decode()
+
     def set_max_blocks(self, max_blocks: int):
         check(lib().smol_csum_tool_set_max_blocks(self._h, int(max_blocks)),
               "smol_csum_tool_set_max_blocks")
