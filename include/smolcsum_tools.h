@@ -38,7 +38,7 @@ int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum
  * 0: 8 x 6, 1: 16 x 3, 2: 16 x 6, 3: 32 x 3, 4: 32 x 4, 5: 64 x 2, 6: 64 x 4, 7: 8 x 7, 8: 16 x 4. */
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
-/* Kernel variant (-1 = automatic: 1 for emit over descriptor batches, 5 otherwise).  The
+/* Kernel variant (-1 = automatic: 7 for emit over descriptor batches, 5 otherwise).  The
  * "walk" kernel (a group parses and finishes its own record) reads 16-byte chunks on a grid that
  * starts at the record's 16-byte boundary: 0 = non-temporal loads + register prefetch of the next
  * step, 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch; or at its

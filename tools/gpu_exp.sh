@@ -4,7 +4,13 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/exp
 mkdir -p $O
-echo "== sweep c3"
-timeout -k 10 600 python tools/sweep.py --config c3 --shapes 0,1,2,4,6,8 --var 1,7 --tile 32 --defer 0 > $O/sweep_c3.log 2>&1 || { echo "rc=$?"; tail -20 $O/sweep_c3.log; exit 1; }
-grep '"round": 1' $O/sweep_c3.log | cut -c1-160
+for rep in 1 2 3; do
+for c in c2 c4; do
+    for lib in new alt; do
+        if [ $lib = alt ]; then export SMOLCSUM_LIB=$PWD/build_alt/libsmolcsum.so; else unset SMOLCSUM_LIB; fi
+        timeout -k 10 300 python bench.py --config $c --cpu-seconds 0 > $O/ab_${c}_${lib}.log 2>&1 || { echo "rc=$?"; tail -20 $O/ab_${c}_${lib}.log; exit 1; }
+        python3 -c "import json; d=json.loads(open('$O/ab_${c}_${lib}.log').read().strip().splitlines()[-1]); print('$rep $c $lib', d['value'], d['kernels_ms'])"
+    done
+done
+done
 echo "== done"
