@@ -50,16 +50,20 @@ def _packet(rng, i):
     return P.ipv6(V6A, V6B, 58, P.icmp_echo(128, pay)), 48
 
 
-def _run(eng, recs, copies_spec, caps=(0, 0, 0, 0, 0), shape=-1, fixed_stride=None, gap_seed=None, seed=0):
+def _run(eng, recs, copies_spec, caps=(0, 0, 0, 0, 0), shape=-1, fixed_stride=None, gap_seed=None, seed=0,
+         fixed_len=None, variant=-1, blocks=0, base=0):
     """recs: list of full packets; copies_spec: list of (dst_offset, len) per record (payload taken
-    from the packet itself).  Returns (device statuses)."""
+    from the packet itself).  Fixed-stride batches: record i at base + i * fixed_stride, fixed_len
+    (default: the stride) bytes, random bytes in the gaps.  Returns (device statuses)."""
     rng = np.random.default_rng(seed)
     n = len(recs)
     if fixed_stride:
-        buf = np.zeros(n * fixed_stride + 16, np.uint8)
-        offs = np.arange(n, dtype=np.uint64) * fixed_stride
-        lens = np.full(n, fixed_stride, np.uint32)
+        L = fixed_len or fixed_stride
+        buf = rng.integers(0, 256, base + n * fixed_stride + 16, dtype=np.uint8)
+        offs = base + np.arange(n, dtype=np.uint64) * fixed_stride
+        lens = np.full(n, L, np.uint32)
         for i, r in enumerate(recs):
+            assert len(r) <= L
             buf[offs[i]:offs[i] + len(r)] = np.frombuffer(r, np.uint8)
     else:
         buf, offs, lens = P.pack(recs, gap_rng=np.random.default_rng(gap_seed) if gap_seed is not None else None)
@@ -92,19 +96,25 @@ def _run(eng, recs, copies_spec, caps=(0, 0, 0, 0, 0), shape=-1, fixed_stride=No
     ref_st = oracle.batch_copy_emit(ref, desc, n, src, copies, caps=caps)
 
     eng.set_shape(shape)
+    eng.set_variant(variant)
+    eng.set_max_blocks(blocks)
     try:
         d = torch.from_numpy(buf.copy()).cuda()
         dsrc = torch.from_numpy(src).cuda()
         dcp = torch.from_numpy(copies.view(np.uint8).copy()).cuda()
         st = torch.zeros(n, dtype=torch.uint8, device="cuda")
         if fixed_stride:
-            batch = E.Batch.fixed(n, fixed_stride, fixed_stride, E.KIND_IP)
+            batch = E.Batch.fixed(n, fixed_stride, fixed_len or fixed_stride, E.KIND_IP)
+            dv = d[base:]
         else:
             batch = E.Batch.from_records(offs, lens, kinds, "cuda:0")
-        eng.copy_emit(d, batch, dsrc, dcp, caps=caps, status=st)
+            dv = d
+        eng.copy_emit(dv, batch, dsrc, dcp, caps=caps, status=st)
         got = d.cpu().numpy()
     finally:
         eng.set_shape(-1)
+        eng.set_variant(-1)
+        eng.set_max_blocks(0)
     diff = np.nonzero(got != ref)[0]
     assert diff.size == 0, f"bytes differ at {diff[:8]} (got {got[diff[:8]]} want {ref[diff[:8]]})"
     assert np.array_equal(st.cpu().numpy(), ref_st)
@@ -122,6 +132,52 @@ def test_copy_emit_fixed_stride_payloads(eng):
     st, got, offs, lens = _run(eng, recs, spec, fixed_stride=1500, seed=2)
     vst = oracle.batch_verify(got.copy(), None, len(recs), 1500, 1500, 1)
     assert ((vst & E.ST_ACCEPT) != 0).all()
+
+
+def _fixed_case(rng, n, L):
+    """Mixed packets that fit L bytes, with copy ranges of every kind (see
+    test_copy_over_fields_and_edge_ranges)."""
+    recs, spec = [], []
+    for i in range(n):
+        r, hdr = _packet(rng, i)
+        r = r[:L] if len(r) > L else r
+        if len(r) < hdr:
+            r, hdr = P.ipv4(V4A, V4B, 17, P.udp(1, 2, P.rand_bytes(rng, L - 28))), 28
+        # the IP / UDP length fields must match the cut packet: rebuild the common case
+        if i % 6 == 0:
+            r = P.ipv4(V4A, V4B, 17, P.udp(1000 + i, 53, P.rand_bytes(rng, min(L, 1500) - 28)))
+            hdr = 28
+        recs.append(r)
+        m = i % 11
+        if m == 0:
+            spec.append((0, len(r)))
+        elif m == 1:
+            spec.append((hdr, 0))
+        elif m == 2:
+            spec.append((hdr, L - hdr + 1))      # does not fit the record: MALFORMED, untouched
+        elif m == 3:
+            spec.append((5, 30))
+        elif m == 4:
+            spec.append((1, L - 1))              # up to the record's last byte
+        elif m == 5:
+            spec.append((hdr, max(0, len(r) - hdr - 3)))  # ends short of the packet
+        else:
+            spec.append((hdr, L - hdr))          # payload to the end of the record
+    return recs, spec
+
+
+@pytest.mark.parametrize("stride,length", [(384, 384), (385, 385), (1500, 1500), (1514, 1514), (2048, 1500),
+                                           (4001, 4001), (700, 400)])
+def test_copy_emit_fixed_stride_mixed(eng, stride, length):
+    """Fixed-stride batches of mixed records with every kind of copy range, at odd strides, gaps
+    between records (random bytes that must survive), a batch base off the line grid, batch sizes
+    around the 32-record workgroup, natural and capped grids."""
+    rng = np.random.default_rng(stride + length)
+    for n, base in ((1, 0), (2, 5), (33, 64), (1029, 3), (2048, 0)):
+        recs, spec = _fixed_case(rng, n, length)
+        for variant, blocks in ((-1, 0), (-1, 7)):
+            _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,
+                 base=base, seed=n + variant)
 
 
 @pytest.mark.parametrize("shape", [-1, 0, 1, 3, 5])

@@ -52,6 +52,67 @@ __global__ __launch_bounds__(256) void rec_copy_full(const uint8_t* src, uint8_t
     }
 }
 
+
+// 16-B chunks, 8 lanes per record (natural grid: one record per group), source bytes funnel-shifted
+// from two aligned 16-B loads like the fused copy-emit.  OWN_LINES: group r writes the 128-B lines
+// whose first byte lies in its record, whole (every destination line written once, by one
+// group); else it writes only [28, 1500) of its record, with byte stores on the two edge chunks
+// (the partial lines the fused kernel leaves today).
+__device__ __forceinline__ u32x4 funnel(const u32x4& lo, const u32x4& hi, uint32_t sh) {
+    const uint32_t q = sh >> 2, b = sh & 3u;
+    auto pick = [&](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+        return q == 0 ? a0 : q == 1 ? a1 : q == 2 ? a2 : a3;
+    };
+    const uint32_t x0 = pick(lo.x, lo.y, lo.z, lo.w), x1 = pick(lo.y, lo.z, lo.w, hi.x);
+    const uint32_t x2 = pick(lo.z, lo.w, hi.x, hi.y), x3 = pick(lo.w, hi.x, hi.y, hi.z);
+    const uint32_t x4 = pick(hi.x, hi.y, hi.z, hi.w);
+    u32x4 r;
+    r.x = __builtin_amdgcn_alignbyte(x1, x0, b);
+    r.y = __builtin_amdgcn_alignbyte(x2, x1, b);
+    r.z = __builtin_amdgcn_alignbyte(x3, x2, b);
+    r.w = __builtin_amdgcn_alignbyte(x4, x3, b);
+    return r;
+}
+
+template <bool OWN_LINES>
+__global__ __launch_bounds__(256) void rec_copy16(const uint8_t* src, uint8_t* dst, uint64_t n) {
+    const int lane = threadIdx.x & 7;
+    const uint64_t r = (uint64_t)blockIdx.x * 32 + threadIdx.x / 8;
+    if (r == 0 || r >= n) return;  // record 0's chunk grid would start before the source
+    const uint64_t d0 = (uint64_t)dst + r * 1500, d1 = d0 + 1500;
+    const uint64_t lo = OWN_LINES ? (r == 0 ? d0 : (d0 + 127) & ~127ull) : d0 + 28;
+    const uint64_t hi = OWN_LINES ? (r + 1 == n ? d1 : (d1 + 127) & ~127ull) : d1;
+    const uint64_t c0 = lo & ~15ull;
+    const uint32_t nch = (uint32_t)((hi - c0 + 15) >> 4);
+    const int64_t sdelta = (int64_t)((uint64_t)src + r * 1472) - (int64_t)(d0 + 28);  // src = dst + sdelta
+    for (uint32_t k0 = 0; k0 < nch; k0 += 32) {
+        u32x4 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + u * 8 + lane;
+            const uint64_t c = c0 + 16ull * (k < nch ? k : 0);
+            const uint64_t sa = (uint64_t)((int64_t)c + sdelta);
+            a[u] = *(const GMEM u32x4*)(sa & ~15ull);
+            b[u] = *(const GMEM u32x4*)((sa & ~15ull) + 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + u * 8 + lane;
+            if (k >= nch) continue;
+            const uint64_t c = c0 + 16ull * k;
+            const uint64_t sa = (uint64_t)((int64_t)c + sdelta);
+            const u32x4 v = funnel(a[u], b[u], (uint32_t)(sa & 15u));
+            if (c >= lo && c + 16 <= hi) {
+                *(GMEM u32x4*)c = v;
+            } else {
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                for (int j = 0; j < 16; ++j)
+                    if (c + j >= lo && c + j < hi) *(GMEM uint8_t*)(c + j) = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+            }
+        }
+    }
+}
+
 int main() {
     const uint64_t bytes = 1500ull << 20;
     uint8_t *a, *b;
@@ -86,6 +147,8 @@ int main() {
     const uint64_t n = 1ull << 20;
     timeit("rec_copy 1472 B -> stride 1500 (+28)", [&] { hipLaunchKernelGGL(rec_copy, dim3(256 * 8), dim3(256), 0, 0, a, b, n); });
     timeit("rec_copy_full 1500 B (all bytes)", [&] { hipLaunchKernelGGL(rec_copy_full, dim3(256 * 8), dim3(256), 0, 0, a, b, n); });
+    timeit("rec_copy16 own lines (whole lines)", [&] { hipLaunchKernelGGL(rec_copy16<true>, dim3(n / 32), dim3(256), 0, 0, a, b, n); });
+    timeit("rec_copy16 [28,1500) (partial edges)", [&] { hipLaunchKernelGGL(rec_copy16<false>, dim3(n / 32), dim3(256), 0, 0, a, b, n); });
     CK(hipGetLastError());
     return 0;
 }
