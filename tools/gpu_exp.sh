@@ -4,8 +4,10 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/exp
 mkdir -p $O
-for v in 1 9 10 11 12 1 9; do
-    timeout -k 10 300 python bench.py --config c2copy --cpu-seconds 0 --variant $v > $O/c2copy_$v.log 2>&1 || { echo "rc=$?"; tail -20 $O/c2copy_$v.log; exit 1; }
-    python3 -c "import json; d=json.loads(open('$O/c2copy_$v.log').read().strip().splitlines()[-1]); print('var $v', d['value'], d['kernels_ms'])"
+for c in c3 c3; do
+    timeout -k 10 600 python tools/sweep.py --config $c --shapes 1,8 --var 5,8 --defer 0 --reps 10 > $O/sweep_$c.log 2>&1 || { echo "rc=$?"; tail -20 $O/sweep_$c.log; exit 1; }
+    grep '"round": 1' $O/sweep_$c.log | cut -c1-170
 done
+echo "== fetch"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc8 -o run -- python3 bench.py --config c2 --steps 5 --warmup 1 --cpu-seconds 0 --variant 8 > $O/pmc8.log 2>&1 || { echo "rc=$?"; tail -20 $O/pmc8.log; exit 1; }
 echo "== done"
