@@ -176,7 +176,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
     // Variants: 0-2, 5-6 = walk kernel (csum_walk.h VarT: load policy, prefetch, chunk
     // grid), 3-4, 7 = tile kernel (csum_tile.hip: nt / plain loads, nt on the line grid), IP emit
-    // and verify only.
+    // and verify only; 8 = walk kernel without prefetch, copy-emit only (its default; other modes
+    // run variant 0 for it).
     int variant = ctx->variant;
     const bool has_desc = b->desc != nullptr;
     if (variant < 0) variant = auto_variant(mode, has_desc);
@@ -190,7 +191,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool two_pass = ctx->defer_emit == 1 && !d_addrs;
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
-        hipError_t e = launch_csum(MODE_COPY, shape, 1, p, ctx->max_blocks, s);
+        hipError_t e = launch_csum(MODE_COPY, shape, ctx->variant == 1 ? 1 : 8, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
     }
@@ -446,7 +447,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 7) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 8) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

@@ -48,12 +48,13 @@
 namespace smolcsum {
 
 // Kernel variants: load cache policy, register prefetch, chunk-grid alignment.
-// 0 = nt + prefetch, 1 = plain + prefetch, 2 = nt without prefetch (16-byte grid);
-// 5 = nt + prefetch, 6 = plain + prefetch (128-byte line grid).  3 / 4 are the tile kernel.
+// 0 = nt + prefetch, 1 = plain + prefetch, 2 = nt without prefetch, 8 = plain without prefetch
+// (16-byte grid); 5 = nt + prefetch, 6 = plain + prefetch (128-byte line grid).  3 / 4 / 7 are the
+// tile kernel.
 template <int VAR>
 struct VarT {
     static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5;
-    static constexpr bool PF = VAR != 2;
+    static constexpr bool PF = VAR != 2 && VAR != 8;
     static constexpr bool LINE = VAR == 5 || VAR == 6;
 };
 
@@ -832,18 +833,27 @@ hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_bl
 
 // MODE_COPY keeps three chunks per lane and step (record + two source chunks), so it is built for
 // the U <= 3 shapes only (wider shapes map to the same group size with fewer chunks) and for the
-// plain-load variant on the 16-byte grid (measured best for emit).
-template <bool IMPLICIT>
-hipError_t launch_copy(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+// plain-load variants on the 16-byte grid.  Without the register prefetch (variant 8, the default)
+// the kernel needs fewer VGPRs and runs more waves per SIMD: C2 copy-emit 0.95 -> 0.85 ms on
+// MI355X (tools/gpu_exp.sh sweep, profiles/r01_kernel_stats_c2copy.csv); variant 1 keeps the
+// prefetch for comparison.
+template <bool IMPLICIT, int VAR>
+hipError_t launch_copy_var(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (shape) {
         case CFG_G8U6:
-        case CFG_G8U7: return launch_one<8, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
+        case CFG_G8U7: return launch_one<8, 3, MODE_COPY, IMPLICIT, VAR>(p, max_blocks, s);
         case CFG_G32U3:
-        case CFG_G32U4: return launch_one<32, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
+        case CFG_G32U4: return launch_one<32, 3, MODE_COPY, IMPLICIT, VAR>(p, max_blocks, s);
         case CFG_G64U2:
-        case CFG_G64U4: return launch_one<64, 2, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
-        default: return launch_one<16, 3, MODE_COPY, IMPLICIT, 1>(p, max_blocks, s);
+        case CFG_G64U4: return launch_one<64, 2, MODE_COPY, IMPLICIT, VAR>(p, max_blocks, s);
+        default: return launch_one<16, 3, MODE_COPY, IMPLICIT, VAR>(p, max_blocks, s);
     }
+}
+
+template <bool IMPLICIT>
+hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    return var == 1 ? launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s)
+                    : launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);
 }
 
 }  // namespace smolcsum

@@ -31,7 +31,7 @@ hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t 
             return implicit ? launch_walk<MODE_EMIT, true>(shape, var, p, max_blocks, s)
                             : launch_walk<MODE_EMIT, false>(shape, var, p, max_blocks, s);
         case MODE_COPY:
-            return implicit ? launch_copy<true>(shape, p, max_blocks, s) : launch_copy<false>(shape, p, max_blocks, s);
+            return implicit ? launch_copy<true>(shape, var, p, max_blocks, s) : launch_copy<false>(shape, var, p, max_blocks, s);
         default:
             return implicit ? launch_walk<MODE_VERIFY, true>(shape, var, p, max_blocks, s)
                             : launch_walk<MODE_VERIFY, false>(shape, var, p, max_blocks, s);

@@ -175,7 +175,7 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
     rng = np.random.default_rng(stride + length)
     for n, base in ((1, 0), (2, 5), (33, 64), (1029, 3), (2048, 0)):
         recs, spec = _fixed_case(rng, n, length)
-        for variant, blocks in ((-1, 0), (-1, 7)):
+        for variant, blocks in ((-1, 0), (-1, 7), (1, 0)):  # default (variant 8) and the prefetch variant
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,
                  base=base, seed=n + variant)
 
