@@ -9,17 +9,25 @@ checksummed = bytes covered by checksum::data spans (IPv4 header + UDP length) o
 wall time, summed over GPUs (weak scaling: every rank owns its own batch; no collective on the
 data path — only barrier + a max-reduction of the elapsed time for reporting).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c2copy]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0 (see the contract in the task description / DESIGN.md §Measurement).
+`--gpus N` without a torch.distributed.run environment starts the N rank processes itself (one per
+GPU, before anything in this process touches a GPU); under torch.distributed.run the world size
+must equal N.  `--dry-run` runs the same launch, rendezvous and reporting on CPU (gloo) with an
+empty step: it checks the multi-rank plumbing, it measures nothing.
+
+Prints ONE JSON line on rank 0 (see the contract in the task description / DESIGN.md §6).
 """
 from __future__ import annotations
 
 import argparse
 import glob
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,9 +41,10 @@ from smoltcp_amd import shard as S  # noqa: E402
 METRIC = "GiB/s checksummed (device-resident), batched 1500B segments, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 GIB = float(1 << 30)
+CPU_SAMPLE_BYTES = 1_600_000_000  # per buffer: larger than any host LLC (EPYC L3 <= 1.1 GB)
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -48,7 +57,55 @@ def parse_args():
     ap.add_argument("--variant", type=int, default=-1, help="force a kernel variant (tuning)")
     ap.add_argument("--defer", type=int, default=-1, help="emit strategy: -1 auto, 0 in-pass, 1 two-pass (tuning)")
     ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch + rendezvous + reporting only, on CPU (gloo), no checksum work")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------------------------
+# Launcher: --gpus N without torch.distributed.run
+# ---------------------------------------------------------------------------------------------
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """Start `args.gpus` copies of this script, one per GPU (RANK = LOCAL_RANK = i), rendezvous on
+    127.0.0.1, and wait for them.  Rank 0 prints the JSON line; this process prints nothing.  No
+    GPU is initialised here: torch.cuda.device_count() only counts the devices.  If one rank
+    fails, the others are stopped (they would wait at a barrier) and its exit code is returned."""
+    n = args.gpus
+    if not args.dry_run:
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) are visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SMOLCSUM_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc, failed_at = 0, None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and failed_at is None:
+            rc, failed_at = bad[0], time.monotonic()
+        if all(c is not None for c in codes):
+            break
+        if failed_at is not None and time.monotonic() - failed_at > 20:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.1)
+    return rc
 
 
 # ---------------------------------------------------------------------------------------------
@@ -125,6 +182,38 @@ class Workload:
         self.est = None
 
 
+# ---------------------------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the oracle on the host cores this process may use
+# ---------------------------------------------------------------------------------------------
+
+
+def host_cpu_share() -> dict:
+    """The host threads this process can actually run: the affinity mask, capped by a cgroup CPU
+    quota when one is set (a container's share of a large host; `nproc` shows the whole host)."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                period = int(f.read())
+            if q > 0:
+                quota = q / period
+        except (OSError, ValueError):
+            pass
+    threads = aff if quota is None else max(1, min(aff, int(math.floor(quota))))
+    if os.environ.get("SMOL_CPU_THREADS"):
+        threads = max(1, int(os.environ["SMOL_CPU_THREADS"]))
+    return {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota, "threads": threads}
+
+
 def _oracle_pass(oracle, tx, rx, desc, m, stride, L, kind, caps, threads, pool):
     """One emit(tx) + verify(rx) pass of the oracle over m records, split over `threads` host
     threads (ctypes releases the GIL inside the C calls).  Returns the verify status array."""
@@ -147,11 +236,12 @@ def _oracle_pass(oracle, tx, rx, desc, m, stride, L, kind, caps, threads, pool):
 
 
 def cpu_baseline(E, wl, seconds: float):
-    """cpu_baseline leg: the oracle (a C restatement of smoltcp's scalar checksum + gates) timed on
-    this host over a bounded sample of the same workload, on 1 thread and on all the host threads
-    this process may use.  The oracle is also the checker here: its emit of the sample (emit is
-    idempotent) must reproduce the device's emitted bytes and its verify the device's status
-    bytes, bit for bit."""
+    """cpu_baseline leg: the oracle (a C restatement of smoltcp's scalar checksum + gates), built on
+    this host with ROCm clang -O3 -march=native, timed over a sample of the same workload larger
+    than the host's last-level cache, on 1 thread and on every host thread this process may use;
+    the value is the median of >= 10 passes.  The oracle is also the checker here: its emit of the
+    sample (emit is idempotent) must reproduce the device's emitted bytes and its verify the
+    device's status bytes, bit for bit."""
     import concurrent.futures as cf
 
     import torch
@@ -160,17 +250,20 @@ def cpu_baseline(E, wl, seconds: float):
 
     if seconds <= 0:
         return None, None
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    share = host_cpu_share()
+    threads = share["threads"]
     if wl.batch.desc is None:
         L = wl.batch.length
-        m = min(wl.n, 8192 * threads)
+        m = min(wl.n, max(1, CPU_SAMPLE_BYTES // L))
         end = (m - 1) * L + L
         desc, stride = None, L
         span = wl.span_bytes * m // wl.n
     else:
-        m = min(wl.n, 2048 * threads)
-        d = wl.batch.desc[: 16 * m].cpu().numpy().view(E.DESC_DTYPE).copy()
-        end = int(d["offset"][-1] + d["len"][-1])
+        d_all = wl.batch.desc.cpu().numpy().view(E.DESC_DTYPE)
+        ends = d_all["offset"] + d_all["len"].astype(np.uint64)
+        m = max(1, int(np.searchsorted(ends, np.uint64(CPU_SAMPLE_BYTES), side="right")))
+        d = d_all[:m].copy()
+        end = int(ends[m - 1])
         desc, stride, L = d, 0, 0
         span = int(d["len"].astype(np.uint64).sum())
     dev_tx = wl.tx[:end].cpu().numpy()
@@ -178,29 +271,31 @@ def cpu_baseline(E, wl, seconds: float):
     tx = dev_tx.copy()
     rx = wl.rx[:end].cpu().numpy().copy()
     caps = (0, 0, 0, 0, 0)
-    oracle.lib()
+    build = oracle.use_native()
     res = {}
     st = None
     with cf.ThreadPoolExecutor(threads) as pool:
         for t in sorted({1, threads}):
-            reps, t0 = 0, time.perf_counter()
-            while True:
+            _oracle_pass(oracle, tx, rx, desc, m, stride, L, wl.kind, caps, t, pool)  # warm
+            times, t0 = [], time.perf_counter()
+            while len(times) < 10 or (time.perf_counter() - t0 < seconds / 2 and len(times) < 200):
+                a = time.perf_counter()
                 st = _oracle_pass(oracle, tx, rx, desc, m, stride, L, wl.kind, caps, t, pool)
-                reps += 1
-                el = time.perf_counter() - t0
-                if el >= seconds / 2:
-                    break
-            res[t] = (2 * span * reps / el / GIB, reps, el)
+                times.append(time.perf_counter() - a)
+            med = float(np.median(times))
+            res[t] = {"GiB/s": 2 * span / med / GIB, "reps": len(times), "median_s": med,
+                      "spread": float((max(times) - min(times)) / med)}
     torch.cuda.synchronize()
     parity = {"records": m, "emit_bitexact": bool(np.array_equal(tx, dev_tx)),
               "verify_bitexact": bool(np.array_equal(st, dev_st)),
               "checker": "oracle/csum_oracle.c on the cpu_baseline sample"}
-    v, reps, el = res[threads]
-    out = {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-           "single_core_value": round(res[1][0], 3),
-           "sample": f"{m} records of the same workload (emit tx + verify rx), {reps} passes in {el:.1f} s on "
-                     f"{threads} threads; oracle/csum_oracle.c (gcc -O3 -march=x86-64-v3), records split "
-                     f"evenly over the threads"}
+    r = res[threads]
+    out = {"value": round(r["GiB/s"], 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "single_core_value": round(res[1]["GiB/s"], 3),
+           "host": share,
+           "sample": f"{m} records of the same workload ({end / 1e9:.2f} GB per buffer, > host LLC): emit tx + "
+                     f"verify rx; median of {r['reps']} passes on {threads} threads ({res[1]['reps']} on 1); "
+                     f"oracle/csum_oracle.c built {build}; records split evenly over the threads"}
     return out, parity
 
 
@@ -218,19 +313,80 @@ def load_traffic(cfg: str, kernel: str):
     return None, None
 
 
-def main():
-    args = parse_args()
+# ---------------------------------------------------------------------------------------------
+# One rank
+# ---------------------------------------------------------------------------------------------
+
+
+def gather_floats(vals, device=None):
+    """all_gather of a few floats per rank -> list (one list per rank); identity at world 1."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [list(vals)]
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.cpu().tolist()] for o in out]
+
+
+def run_dry(args, world, rank, local):
+    """--dry-run: the launch, rendezvous and reporting of a multi-rank run, on CPU, no work."""
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    mine = time.perf_counter() - t0
+    per = gather_floats([rank, local, mine])
+    elapsed = S.max_over_ranks(mine)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 6),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                          "data": "dry run: no checksum work", "dry_run": True,
+                          "config": {"workload": f"dry run of --config {args.config}",
+                                     "parallelism": f"shard x{world} (no collective)"},
+                          "per_rank": [{"rank": int(p[0]), "local_rank": int(p[1]), "elapsed_s": p[2]} for p in per]}),
+              flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    world, rank, local = S.dist_env()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.dry_run:
+        run_dry(args, world, rank, local)
+        return 0
+
     import torch
     import torch.distributed as dist
 
     from smoltcp_amd import engine as E
 
-    world, rank, local = S.dist_env()
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if torch.cuda.device_count() <= local:
+        print(f"bench.py: rank {rank} needs cuda:{local}, {torch.cuda.device_count()} GPU(s) visible",
+              file=sys.stderr)
+        return 2
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     eng = E.ChecksumEngine(local)
     if args.shape >= 0:
@@ -270,9 +426,10 @@ def main():
     for i in range(args.steps):
         step()
     torch.cuda.synchronize()
+    mine = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = S.max_over_ranks(time.perf_counter() - t0, device=dev)
+    elapsed = S.max_over_ranks(mine, device=dev)
 
     # Kernel durations for the roofline: K more steps with HIP events at the kernel boundaries, on
     # the stream the kernels are launched on.
@@ -284,9 +441,10 @@ def main():
     emit_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     verify_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
 
-    # correctness of the last verify against the oracle on a sample (and the expected rejections)
+    # the expected rejections of the last verify (1/64 single-bit flips, or none for C5)
     st = wl.status.cpu().numpy()
     rejected = int(((st & E.ST_ACCEPT) == 0).sum())
+    per = gather_floats([rank, local, mine, emit_ms, verify_ms, rejected], device=dev)
 
     probe = None
     if args.probe and rank == 0:
@@ -343,6 +501,10 @@ def main():
         achieved = kd["bytes"] / (kd["ms"] * 1e-3) / 1e9
         dop = "copy_emit" if (wl.copy is not None and dom == "emit") else dom
         traffic, tsrc = load_traffic(args.config, dop)
+        per_rank = [{"rank": int(p[0]), "local_rank": int(p[1]), "elapsed_s": round(p[2], 6),
+                     "value": round(2 * wl.span_bytes * args.steps / p[2] / GIB, 2),
+                     "ms_per_step": round(p[2] / args.steps * 1e3, 4), "emit_ms": round(p[3], 4),
+                     "verify_ms": round(p[4], 4), "verify_rejected": int(p[5])} for p in per]
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -370,6 +532,7 @@ def main():
             "kernel_timing": "HIP events at the kernel boundaries on the launch stream, over a second pass of "
                              "K steps after the timed region (the timed region has no events between kernels)",
             "verify_rejected": rejected,
+            "per_rank": per_rank,
             "cpu_baseline": cpu,
             "parity_sample": parity,
         }
@@ -381,7 +544,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

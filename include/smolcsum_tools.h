@@ -45,7 +45,10 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
  * 128-byte line boundary: 5 = non-temporal loads + prefetch, 6 = plain loads + prefetch.
  * 3 / 4 = the "tile" kernel (groups only stream and sum, lanes finish 64 records at once) with
  * non-temporal / plain loads on the 16-byte grid, 7 = the tile kernel with non-temporal loads on
- * the line grid — emit and verify only (data() uses the walk kernel). */
+ * the line grid — emit and verify only (data() uses the walk kernel).  8 = the walk kernel on the
+ * 16-byte grid with plain loads and no prefetch (copy-emit's default).  9 / 10 = variant 5 with the
+ * first two / the first 16-byte chunk of every lane's step loaded cached, so that the lines holding
+ * the fields are resident in L2 when emit stores them (fixed-stride emit only; elsewhere 5). */
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
 
 /* Tile kernel: records per wavefront tile, 32 (default) or 64. */
@@ -62,7 +65,9 @@ int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int mode);
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
 
 /* Read-only HBM streaming probe over `bytes` (multiple of 16, 16-byte aligned `d_buf`): the
- * achievable read ceiling that the checksum kernels are compared with.  `d_sink` is one u32. */
+ * achievable read ceiling that the checksum kernels are compared with.  Each wavefront streams
+ * contiguous 8-KiB pieces with eight non-temporal 16-byte loads per lane in flight (the fastest
+ * pattern of tools/probe_bw.hip), 8 workgroups per CU.  `d_sink` is one u32. */
 int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint64_t bytes,
                                uint32_t* d_sink, void* stream);
 

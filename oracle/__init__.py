@@ -51,7 +51,34 @@ def lib() -> ctypes.CDLL:
     path = os.path.join(_HERE, "liboracle.so")
     if not os.path.exists(path):
         build()
-    L = ctypes.CDLL(path)
+    _LIB = _bind(ctypes.CDLL(path))
+    return _LIB
+
+
+NATIVE_CC = "/opt/rocm/lib/llvm/bin/clang"
+
+
+def use_native() -> str:
+    """bench.py's cpu_baseline: rebuild this restatement for the host it runs on (ROCm clang -O3
+    -march=native) into a temporary directory and use it from now on.  Falls back
+    to the committed recipe's build (gcc -O3 -march=x86-64-v3) if the compiler is missing.
+    Returns a description of the build in use."""
+    global _LIB
+    import tempfile
+
+    out = os.path.join(tempfile.mkdtemp(prefix="smol_oracle_"), "liboracle_native.so")
+    cmd = [NATIVE_CC, "-O3", "-march=native", "-fPIC", "-shared", "-std=c11", "-o", out,
+           os.path.join(_HERE, "csum_oracle.c")]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=120)
+        _LIB = _bind(ctypes.CDLL(out))
+        return "with ROCm clang -O3 -march=native on this host"
+    except (OSError, subprocess.SubprocessError):
+        lib()
+        return "with gcc -O3 -march=x86-64-v3 (oracle/Makefile; ROCm clang unavailable)"
+
+
+def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     u8p = ctypes.c_void_p
     L.oracle_data.argtypes = [u8p, ctypes.c_size_t]
     L.oracle_data.restype = ctypes.c_uint16
@@ -113,7 +140,6 @@ def lib() -> ctypes.CDLL:
         f.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, u8p,
                       ctypes.POINTER(CapsC), u8p]
         f.restype = None
-    _LIB = L
     return L
 
 

@@ -96,7 +96,7 @@ constexpr uint32_t kNaturalGrid = 0x7fffffffu;
 int walk_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 1 : 5; }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : 5; }
 
-bool line_grid(int variant) { return variant == 5 || variant == 6; }
+bool line_grid(int variant) { return variant == 5 || variant == 6 || variant == 9 || variant == 10; }
 
 int auto_shape(uint32_t len, bool has_desc, bool line = false) {
     if (has_desc) return CFG_G16U3;
@@ -447,7 +447,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 8) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 10) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

@@ -1,4 +1,5 @@
-// Tile kernel: batched emit / verify for MI355X (gfx950), the default engine.
+// Tile kernel: batched emit / verify for MI355X (gfx950).  The library's default only for emit over
+// descriptor batches (C3; csum_api.cpp auto_variant); every other call runs the walk kernel.
 //
 // A wavefront owns a TILE of 32 or 64 consecutive records and works on it in three phases:
 //

@@ -51,11 +51,15 @@ namespace smolcsum {
 // 0 = nt + prefetch, 1 = plain + prefetch, 2 = nt without prefetch, 8 = plain without prefetch
 // (16-byte grid); 5 = nt + prefetch, 6 = plain + prefetch (128-byte line grid).  3 / 4 / 7 are the
 // tile kernel.
+// 9 / 10 = variant 5 with the first two / the first chunk of every lane's step loaded cached
+// (fixed-stride emit only: the 128-B line(s) holding the two fields stay resident in L2 when the
+// field stores arrive; measured in DESIGN.md §5).
 template <int VAR>
 struct VarT {
-    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5;
+    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10;
     static constexpr bool PF = VAR != 2 && VAR != 8;
-    static constexpr bool LINE = VAR == 5 || VAR == 6;
+    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10;
+    static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
 };
 
 template <bool LINE>
@@ -148,7 +152,7 @@ struct Regs<U, true> {
 // payload bytes (so no load ever leaves the source range's aligned chunks).
 // Chunks at addresses >= lim are not loaded (they come from the next record's LDS window, see
 // shared_from).
-template <int G, int U, bool NT, bool COPY, bool LINE>
+template <int G, int U, bool NT, bool COPY, bool LINE, int CACHED_U = 0>
 __device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, uint32_t nch,
                                           uint32_t step, int lane, bool valid, uint64_t dummy,
                                           uint64_t lim = ~0ull) {
@@ -159,7 +163,8 @@ __device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, ui
         const uint32_t k = step * (G * U) + u * G + lane;
         const bool in = valid && k < nch && base + 16ull * k < lim;
         if constexpr (!COPY) {
-            R.v[u] = ld16<NT>((gcv4)(in ? base + 16ull * k : dummy));
+            const gcv4 q = (gcv4)(in ? base + 16ull * k : dummy);
+            R.v[u] = u < CACHED_U ? ld16<false>(q) : ld16<NT>(q);  // folds per unrolled u
         } else {
             const int64_t pos = (int64_t)(16u * k) - (int64_t)(rr.a0 & 15u);  // record offset of the chunk
             const bool full = pos >= (int64_t)rr.p0 && pos + 16 <= (int64_t)rr.p1;
@@ -501,7 +506,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
-template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC>
+template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           uint32_t* gsh, int gib) {
@@ -520,8 +525,8 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     // SKIPD: no prefetch when the group has nothing left (one record per group in a natural grid:
     // every record's last step would otherwise issue U loads of the dummy line)
     if (PF && (!SKIPD || have2))
-        load_step<G, U, NT, COPY, LINE>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
-                                        shared_from<G, MODE, IMPLICIT, LINE>(p, r2, rec2.a0, gib, ngroups));
+        load_step<G, U, NT, COPY, LINE, CU>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
+                                            shared_from<G, MODE, IMPLICIT, LINE>(p, r2, rec2.a0, gib, ngroups));
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
@@ -685,6 +690,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool NT = VarT<VAR>::NT;
     constexpr bool PF = VarT<VAR>::PF;
     constexpr bool LINE = VarT<VAR>::LINE;
+    constexpr int CU = VarT<VAR>::CACHED_U;
     // Fixed-stride batches: no prefetch once the group has nothing left (one record per group in
     // a natural grid), measured 1-1.5 % faster (C2 verify 0.2444 -> 0.2422 ms, C4 0.2219 -> 0.2189
     // ms).  Descriptor batches keep the unconditional prefetch: there the conditional load made
@@ -714,12 +720,12 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     Regs<U, COPY> va;
     if (PF) {
         Regs<U, COPY> vb;
-        load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
-                                        shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
+        load_step<G, U, NT, COPY, LINE, CU>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
+                                            shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC>(p, w, va, vb, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC>(p, w, vb, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU>(p, w, va, vb, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU>(p, w, vb, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
         }
     } else {
         while (true) {
@@ -811,6 +817,13 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 2: return launch_shape<MODE, IMPLICIT, 2>(shape, p, max_blocks, s);
         case 5: return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
+        case 9:
+        case 10:
+            if constexpr (MODE == MODE_EMIT && IMPLICIT) {
+                return var == 9 ? launch_shape<MODE, IMPLICIT, 9>(shape, p, max_blocks, s)
+                                : launch_shape<MODE, IMPLICIT, 10>(shape, p, max_blocks, s);
+            }
+            return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         default: return launch_shape<MODE, IMPLICIT, 0>(shape, p, max_blocks, s);
     }
 }

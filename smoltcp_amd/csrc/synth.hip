@@ -204,20 +204,32 @@ hipError_t launch_corrupt(const SynthParams& p, uint32_t every, hipStream_t s) {
 
 namespace smolcsum {
 
-// Read-only HBM streaming probe: every lane reads 16-byte chunks with a grid stride and folds
-// them into a value that is stored only if it hits an impossible pattern (keeps the loads live).
+// Read-only HBM streaming probe (the achievable read ceiling): each wavefront streams contiguous
+// 8-KiB pieces (8 non-temporal 16-byte loads per lane in flight, lane-contiguous), grid stride over
+// the pieces, then the < 8 KiB tail with a plain grid stride.  Loads are summed into a value stored
+// only if it hits an impossible pattern (keeps them live).  tools/probe_bw.hip `wave_spans U8 nt`.
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void stream_read_kernel(const uint4* p, uint64_t n16, uint32_t* sink) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int UNR = 8;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const uint64_t per = 64ull * UNR;
+    const u32x4s* q = reinterpret_cast<const u32x4s*>(p);
     uint32_t acc = 0;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
-        acc += (a.x ^ b.y) + (c.z ^ d.w) + (a.w ^ d.x) + (b.z ^ c.y);
+    for (uint64_t base = w0 * per; base + per <= n16; base += nw * per) {
+        u32x4s v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) v[u] = __builtin_nontemporal_load(q + base + u * 64 + lane);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+            acc += __builtin_amdgcn_sad_u16(v[u].x, 0, 0) + __builtin_amdgcn_sad_u16(v[u].y, 0, 0) +
+                   __builtin_amdgcn_sad_u16(v[u].z, 0, 0) + __builtin_amdgcn_sad_u16(v[u].w, 0, 0);
     }
-    for (; i < n16; i += stride) {
-        const uint4 a = p[i];
-        acc += a.x ^ a.y ^ a.z ^ a.w;
-    }
+    const uint64_t tail = n16 / per * per;
+    for (uint64_t i = tail + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        acc += p[i].x;
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 

@@ -1,0 +1,71 @@
+"""bench.py's multi-rank launch: `--gpus N` starts N rank processes itself (before any GPU call),
+rendezvous on 127.0.0.1 and rank 0 reports every rank.  `--dry-run` runs that launch,
+rendezvous (gloo) and reporting on CPU with an empty step, so the N > 1 path of the driver's
+scaling run is exercised here without a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout,
+                          env=env, cwd=ROOT)
+
+
+def _json_line(out: str):
+    lines = [ln for ln in out.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_dry_run_launches_n_ranks(n):
+    r = _run(["--gpus", str(n), "--dry-run", "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == n and d["dry_run"] is True
+    assert sorted(p["rank"] for p in d["per_rank"]) == list(range(n))
+    assert sorted(p["local_rank"] for p in d["per_rank"]) == list(range(n))  # one GPU per rank
+    assert d["steps"] == 3 and d["warmup"] == 1
+
+
+def test_dry_run_c5_config():
+    r = _run(["--gpus", "2", "--dry-run", "--config", "c5", "--steps", "2"])
+    assert r.returncode == 0, r.stderr
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and "c5" in d["config"]["workload"]
+
+
+def test_world_size_must_match_gpus():
+    """Under torch.distributed.run (WORLD_SIZE set) a mismatching --gpus is refused."""
+    r = _run(["--gpus", "2", "--dry-run"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr
+
+
+def test_too_few_gpus_fails_loudly():
+    """Without --dry-run the launcher counts the GPUs first (none in this container)."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this host has GPUs")
+    r = _run(["--gpus", "2", "--steps", "1"])
+    assert r.returncode == 2
+    assert "GPU(s) are visible" in r.stderr
+
+
+def test_host_cpu_share():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    s = bench.host_cpu_share()
+    assert s["threads"] >= 1 and s["nproc"] >= 1 and s["threads"] <= s["affinity"]
