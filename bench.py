@@ -55,7 +55,6 @@ def parse_args(argv=None):
                     help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
     ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
     ap.add_argument("--variant", type=int, default=-1, help="force a kernel variant (tuning)")
-    ap.add_argument("--defer", type=int, default=-1, help="emit strategy: -1 auto, 0 in-pass, 1 two-pass (tuning)")
     ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch + rendezvous + reporting only, on CPU (gloo), no checksum work")
@@ -393,8 +392,6 @@ def main(argv=None):
         eng.set_shape(args.shape)
     if args.variant >= 0:
         eng.set_variant(args.variant)
-    if args.defer >= 0:
-        eng.set_deferred_emit(args.defer)
     wl = Workload(E, eng, args.config, args.n, rank, dev)
     torch.cuda.synchronize()
 

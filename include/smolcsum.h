@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SMOLCSUM_ABI_VERSION 2
+#define SMOLCSUM_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------------------------ */
 enum {
@@ -164,12 +164,6 @@ typedef struct smol_csum_ctx smol_csum_ctx_t;
 int smol_csum_ctx_create(int device, smol_csum_ctx_t** out);
 int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx);
 
-/* Reserve the two-pass emit workspace for batches of up to `max_records` records (136 bytes per
- * record, capped at 2^20 records; larger batches are processed in chunks).  Only needed with the
- * two-pass emit (smol_csum_tool_set_deferred_emit): its first call would otherwise allocate
- * device memory, which must not happen inside a HIP graph capture. */
-int smol_csum_ctx_reserve(smol_csum_ctx_t* ctx, uint64_t max_records);
-
 /* checksum::data() over every record span; d_out[i] = data(record i) (u16, numeric value as the
  * reference returns it).  Record kinds are ignored: every record is a raw span. */
 int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
@@ -177,9 +171,11 @@ int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
 
 /* In-place emit: for every record write the IPv4 header checksum and the L4 checksum the way the
  * reference's Repr::emit does under `caps` (fill when tx(), else 0; UDP 0 -> 0xffff; IGMP always
- * filled).  `d_status` (nullable) receives SMOL_ST_MALFORMED / SMOL_ST_UNSUPPORTED per record.
- * One kernel on `stream` (or, when selected with smol_csum_tool_set_deferred_emit, a read pass
- * into the context's workspace plus a write pass); records must not overlap. */
+ * filled).  An ICMPv4 DstUnreachable / TimeExceeded message's embedded IPv4 header gets its header
+ * checksum first, under caps.ipv4, as Icmpv4Repr::emit writes it with Ipv4Repr::emit
+ * (src/wire/icmpv4.rs:520-543).  `d_status` (nullable) receives SMOL_ST_MALFORMED /
+ * SMOL_ST_UNSUPPORTED per record.  One kernel on `stream`; records must not overlap.  No device
+ * memory is allocated: the calls may be captured in a HIP graph. */
 int smol_csum_batch_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                          const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
 

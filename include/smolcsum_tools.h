@@ -54,13 +54,6 @@ int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
 /* Tile kernel: records per wavefront tile, 32 (default) or 64. */
 int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records);
 
-/* Emit strategy: 1 = two passes (the read pass records each record's field writes — for
- * fixed-stride batches on the line grid also the whole 64-B line(s) holding the fields — and a
- * scatter pass writes them afterwards: whole lines need no HBM read-modify-write), 0 = 2-byte
- * field stores inside the read pass, -1 = automatic (the default: in-pass stores, measured
- * faster). */
-int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int mode);
-
 /* Cap the number of workgroups per launch (0 = automatic: CUs x 8). */
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
 

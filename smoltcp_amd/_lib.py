@@ -26,14 +26,13 @@ ERROR_NAMES = {
 ABI_SYMBOLS = [
     "smol_csum_data", "smol_csum_combine", "smol_csum_pseudo_header_v4",
     "smol_csum_pseudo_header_v6", "smol_csum_pseudo_header", "smol_csum_ctx_create",
-    "smol_csum_ctx_destroy", "smol_csum_ctx_reserve", "smol_csum_batch_data", "smol_csum_batch_emit",
+    "smol_csum_ctx_destroy", "smol_csum_batch_data", "smol_csum_batch_emit",
     "smol_csum_batch_verify", "smol_csum_batch_copy_emit", "smol_csum_batch_nhc_udp_emit",
     "smol_csum_batch_nhc_udp_verify", "smol_csum_last_error", "smol_csum_abi_version",
 ]
 TOOL_SYMBOLS = [
     "smol_csum_tool_synth", "smol_csum_tool_corrupt", "smol_csum_tool_set_shape",
-    "smol_csum_tool_set_variant", "smol_csum_tool_set_deferred_emit",
-    "smol_csum_tool_set_tile",
+    "smol_csum_tool_set_variant", "smol_csum_tool_set_tile",
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
     "smol_csum_tool_kernel_name",
 ]
@@ -101,10 +100,6 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_ctx_create.restype = i32
     L.smol_csum_ctx_destroy.argtypes = [vp]
     L.smol_csum_ctx_destroy.restype = i32
-    L.smol_csum_ctx_reserve.argtypes = [vp, u64]
-    L.smol_csum_ctx_reserve.restype = i32
-    L.smol_csum_tool_set_deferred_emit.argtypes = [vp, i32]
-    L.smol_csum_tool_set_deferred_emit.restype = i32
     L.smol_csum_batch_data.argtypes = [vp, vp, ctypes.POINTER(BatchC), vp, vp]
     L.smol_csum_batch_data.restype = i32
     L.smol_csum_batch_emit.argtypes = [vp, vp, ctypes.POINTER(BatchC), ctypes.POINTER(Caps), vp, vp]

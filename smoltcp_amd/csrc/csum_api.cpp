@@ -22,10 +22,6 @@ struct smol_csum_ctx {
     int shape;            // -1 automatic, else CFG_*
     int variant;          // kernel variant (-1 automatic; csum_walk.h VarT, 3/4 tile kernel)
     uint8_t* dummy;       // 256 zero bytes on the device (target of loads with nothing to read)
-    int defer_emit;       // -1 automatic, 0 field stores in the read pass, 1 two-pass emit
-    uint64_t* patch;      // two-pass emit workspace: one meta word per record of a chunk
-    uint8_t* lines;       // two-pass emit workspace: one 128-B line slot per record of a chunk
-    uint64_t patch_cap;   // records the workspace holds
     int tile_records;     // tile kernel: records per wavefront tile (32 or 64)
     bool max_blocks_set;  // grid cap given explicitly (tooling)
 };
@@ -64,13 +60,6 @@ struct DeviceGuard {  // run on ctx->device, restore the caller's current device
         if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
     }
 };
-
-inline uint16_t fold_u32(uint32_t w) {  // propagate_carries, src/wire/ip.rs:767-770
-    uint32_t s = (w >> 16) + (w & 0xffffu);
-    return (uint16_t)(((s >> 16) + s) & 0xffffu);
-}
-
-inline uint16_t swap16(uint16_t v) { return (uint16_t)((v >> 8) | (v << 8)); }
 
 bool caps_valid(const smol_checksum_caps_t* c) {
     if (!c) return false;
@@ -122,30 +111,6 @@ int check_batch(const smol_csum_batch_t* b, const void* d_buf) {
     return SMOL_OK;
 }
 
-// Two-pass emit workspace: records per chunk (8-B meta word + 128-B line slot each: 136 MiB).
-constexpr uint64_t SMOL_EMIT_CHUNK = 1ull << 20;
-constexpr uint64_t kLineSlot = 128;
-
-int reserve_patch(smol_csum_ctx_t* ctx, uint64_t n) {
-    if (n <= ctx->patch_cap) return SMOL_OK;
-    DeviceGuard guard(ctx->device);
-    if (ctx->patch) (void)hipFree(ctx->patch);
-    if (ctx->lines) (void)hipFree(ctx->lines);
-    ctx->patch = nullptr;
-    ctx->lines = nullptr;
-    ctx->patch_cap = 0;
-    hipError_t e = hipMalloc(&ctx->patch, n * sizeof(uint64_t));
-    if (e == hipSuccess) e = hipMalloc(&ctx->lines, n * kLineSlot);
-    if (e != hipSuccess) {
-        if (ctx->patch) (void)hipFree(ctx->patch);
-        ctx->patch = nullptr;
-        ctx->lines = nullptr;
-        return hip_fail(e, "hipMalloc (emit workspace)");
-    }
-    ctx->patch_cap = n;
-    return SMOL_OK;
-}
-
 int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t* b,
         const smol_checksum_caps_t* caps, uint16_t* d_out, uint8_t* d_status, void* stream,
         const uint8_t* d_src = nullptr, const smol_csum_copy_t* d_copy = nullptr,
@@ -185,47 +150,19 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     if (tile_var && (mode == MODE_DATA || mode == MODE_COPY || d_addrs)) variant = walk_variant(mode, has_desc);
     const bool use_tile = variant == 3 || variant == 4 || variant == 7;
     int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, has_desc, line_grid(variant));
-    // Two-pass emit only on request: it trades the in-pass 2-byte stores for a meta word + line
-    // slot per record and a scatter pass, and measured slower (C2: read pass 0.301 ms + scatter
-    // 0.047 ms against 0.315 ms in one pass; the slot writes alone cost 0.049 ms).
-    const bool two_pass = ctx->defer_emit == 1 && !d_addrs;
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
         hipError_t e = launch_csum(MODE_COPY, shape, ctx->variant == 1 ? 1 : 8, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
     }
-    if (use_tile && !(mode == MODE_EMIT && two_pass)) {
+    if (use_tile) {
         hipError_t e = launch_tile(mode, shape, variant == 7 ? 2 : variant - 3, ctx->tile_records, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         return SMOL_OK;
     }
-    if (use_tile) variant = 0;
-    if (mode != MODE_EMIT || !two_pass) {
-        hipError_t e = launch_csum(mode, shape, variant, p, ctx->max_blocks, s);
-        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
-        return SMOL_OK;
-    }
-    // Two-pass emit: read pass -> meta words (+ line slots), then the scatter pass, in chunks of at
-    // most SMOL_EMIT_CHUNK records (the workspace is reserved once per context).  The first record
-    // of a chunk hands over lines only when they lie inside it (the scatter pass cannot see the
-    // previous chunk's meta words).
-    const uint64_t cap = b->n < SMOL_EMIT_CHUNK ? b->n : SMOL_EMIT_CHUNK;
-    int rc = reserve_patch(ctx, cap);
-    if (rc != SMOL_OK) return rc;
-    for (uint64_t start = 0; start < b->n; start += cap) {
-        KParams q = p;
-        q.n = (b->n - start) < cap ? (b->n - start) : cap;
-        if (b->desc) q.desc = b->desc + start;
-        else q.buf = d_buf + start * b->stride;
-        if (d_status) q.status = d_status + start;
-        q.patch = ctx->patch;
-        q.lines = ctx->lines;
-        hipError_t e = launch_csum(MODE_EMIT, shape, variant, q, ctx->max_blocks, s);
-        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
-        e = launch_scatter(q, ctx->max_blocks, s);
-        if (e != hipSuccess) return hip_fail(e, "scatter kernel launch");
-    }
+    hipError_t e = launch_csum(mode, shape, variant, p, ctx->max_blocks, s);
+    if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
     return SMOL_OK;
 }
 
@@ -233,58 +170,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
 
 extern "C" {
 
-// ---- scalar host mirrors --------------------------------------------------------------------
-
-// checksum::data, src/wire/ip.rs:773-804.  Little-endian u16 words are summed exactly in 64 bits
-// and truncated to 32 bits, which equals the reference's wrapping u32 accumulator.
-uint16_t smol_csum_data(const uint8_t* d, size_t n) {
-    uint64_t acc = 0;
-    size_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-        uint64_t q;
-        std::memcpy(&q, d + i, 8);
-        acc += (q & 0xffffu) + ((q >> 16) & 0xffffu) + ((q >> 32) & 0xffffu) + (q >> 48);
-    }
-    for (; i + 2 <= n; i += 2) acc += (uint32_t)d[i] | ((uint32_t)d[i + 1] << 8);
-    if (i < n) acc += d[i];
-    return swap16(fold_u32((uint32_t)acc));
-}
-
-// checksum::combine, src/wire/ip.rs:807-813
-uint16_t smol_csum_combine(const uint16_t* c, size_t n) {
-    uint32_t acc = 0;
-    for (size_t i = 0; i < n; i++) acc += c[i];
-    return fold_u32(acc);
-}
-
-static uint16_t pseudo(const uint8_t* src, const uint8_t* dst, size_t alen, uint8_t nh,
-                       uint32_t length) {
-    const uint8_t pl[4] = {0, nh, (uint8_t)(length >> 8), (uint8_t)length};
-    const uint16_t parts[3] = {smol_csum_data(src, alen), smol_csum_data(dst, alen),
-                               smol_csum_data(pl, 4)};
-    return smol_csum_combine(parts, 3);
-}
-
-// checksum::pseudo_header_v4, src/wire/ip.rs:816-831
-uint16_t smol_csum_pseudo_header_v4(const uint8_t src[4], const uint8_t dst[4], uint8_t nh,
-                                    uint32_t length) {
-    return pseudo(src, dst, 4, nh, length);
-}
-
-// checksum::pseudo_header_v6, src/wire/ip.rs:834-849
-uint16_t smol_csum_pseudo_header_v6(const uint8_t src[16], const uint8_t dst[16], uint8_t nh,
-                                    uint32_t length) {
-    return pseudo(src, dst, 16, nh, length);
-}
-
-// checksum::pseudo_header, src/wire/ip.rs:851-869
-int smol_csum_pseudo_header(int src_family, const uint8_t* src, int dst_family,
-                            const uint8_t* dst, uint8_t nh, uint32_t length, uint16_t* out) {
-    if (!src || !dst || !out || src_family != dst_family) return SMOL_EINVAL;
-    if (src_family == 4) { *out = smol_csum_pseudo_header_v4(src, dst, nh, length); return SMOL_OK; }
-    if (src_family == 6) { *out = smol_csum_pseudo_header_v6(src, dst, nh, length); return SMOL_OK; }
-    return SMOL_EINVAL;
-}
+// The scalar host mirrors (smol_csum_data, _combine, _pseudo_header*) are in csum_scalar.cpp.
 
 // ---- context ---------------------------------------------------------------------------------
 
@@ -316,12 +202,8 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
         return SMOL_ENOMEM;
     }
     c->dummy = dummy;
-    c->defer_emit = -1;
     c->tile_records = 32;
     c->max_blocks_set = false;
-    c->lines = nullptr;
-    c->patch = nullptr;
-    c->patch_cap = 0;
     c->device = device;
     c->num_cu = cus;
     c->max_blocks = kNaturalGrid;
@@ -331,18 +213,11 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     return SMOL_OK;
 }
 
-int smol_csum_ctx_reserve(smol_csum_ctx_t* ctx, uint64_t max_records) {
-    if (!ctx) return SMOL_EINVAL;
-    return reserve_patch(ctx, max_records < SMOL_EMIT_CHUNK ? max_records : SMOL_EMIT_CHUNK);
-}
-
 int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
     if (!ctx) return SMOL_OK;
     {
         DeviceGuard guard(ctx->device);
         (void)hipFree(ctx->dummy);
-        if (ctx->patch) (void)hipFree(ctx->patch);
-        if (ctx->lines) (void)hipFree(ctx->lines);
     }
     delete ctx;
     return SMOL_OK;
@@ -458,12 +333,6 @@ int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records) {
     return SMOL_OK;
 }
 
-int smol_csum_tool_set_deferred_emit(smol_csum_ctx_t* ctx, int mode) {
-    if (!ctx || mode < -1 || mode > 1) return SMOL_EINVAL;
-    ctx->defer_emit = mode;
-    return SMOL_OK;
-}
-
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks) {
     if (!ctx) return SMOL_EINVAL;
     ctx->max_blocks = max_blocks ? max_blocks : kNaturalGrid;
@@ -488,8 +357,7 @@ int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
 const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int has_desc) {
     if (!ctx || op < MODE_DATA || op > MODE_COPY) return "";
     const int v = ctx->variant >= 0 ? ctx->variant : auto_variant(op, has_desc != 0);
-    const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY) &&
-                      !(op == MODE_EMIT && ctx->defer_emit == 1);
+    const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY);
     return tile ? "csum_tile_kernel" : "csum_kernel";
 }
 

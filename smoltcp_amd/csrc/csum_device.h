@@ -72,7 +72,27 @@ struct Geom {
     uint32_t l4_len;     // L4 buffer length
     uint32_t span_end;   // end of the summed L4 span (UDP: l4_off + UDP length field)
     uint32_t fo;         // checksum field offset inside the L4 header (NHC UDP: in the record)
+    uint32_t in_off;     // emit: the IPv4 header embedded in an ICMPv4 DstUnreachable /
+    uint32_t in_hl;      // TimeExceeded message (record offset, length; 0 = none)
 };
+
+// Icmpv6Packet::check_len, src/wire/icmpv6.rs:274-338: the bytes a message of type t needs
+// (max(HEADER_END, header_len()), :296 and header_len :397-418), or 0 when check_len rejects the
+// type outright (Message::Unknown, and RplControl, whose proto-rpl feature is not in the default
+// feature set, Cargo.toml:104-112).
+__host__ __device__ __forceinline__ uint32_t icmpv6_min_len(uint32_t t) {
+    switch (t) {
+        case 0x01: case 0x02: case 0x03: case 0x04:  // DstUnreachable, PktTooBig, TimeExceeded, ParamProblem
+        case 0x80: case 0x81:                        // EchoRequest, EchoReply
+        case 0x85:                                   // RouterSolicit
+        case 0x8f: return 8;                         // MldReport
+        case 0x86: return 16;                        // RouterAdvert (RETRANS_TM.end)
+        case 0x87: case 0x88: return 24;             // NeighborSolicit / NeighborAdvert (TARGET_ADDR.end)
+        case 0x89: return 40;                        // Redirect (DEST_ADDR.end)
+        case 0x82: return 28;                        // MldQuery (QUERY_NUM_SRCS.end)
+        default: return 0;
+    }
+}
 
 // Record geometry: how smoltcp's iface reaches the checksum gates.  Mirrors, check for check,
 //   Ethernet  src/iface/interface/ethernet.rs:4-46
@@ -83,7 +103,11 @@ struct Geom {
 //             src/wire/ipv6ext_header.rs:55-69), next header dispatch :323-366
 //   L4        UdpPacket::check_len udp.rs:57-69, TcpPacket::check_len tcp.rs:155-167,
 //             Icmpv4Packet::check_len icmpv4.rs:207-214, IgmpPacket::check_len igmp.rs:73-80,
-//             the generic len >= 4 of Icmpv6Packet::check_len icmpv6.rs:275-280.
+//             Icmpv6Packet::check_len icmpv6.rs:274-338 (verify: the message-type lengths of
+//             icmpv6_min_len; emit: the generic len >= 4 — Icmpv6Packet::fill_checksum fills any type).
+//   ICMPv4 errors (emit): Icmpv4Repr::emit writes the embedded IPv4 header of DstUnreachable /
+//             TimeExceeded with Ipv4Repr::emit under the same caps (icmpv4.rs:520-543), so its header
+//             checksum is filled (or zeroed) before the ICMP checksum covers it.
 //   6LoWPAN NHC UDP (KIND_NHC_UDP): UdpNhcPacket::check_len nhc.rs:486-500 and the dispatch test of
 //             UdpNhcRepr::parse :701-703; the payload follows the inline checksum if any, and on
 //             emit always an inline checksum (payload_mut :622-626).
@@ -196,12 +220,24 @@ __device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint3
             g.fo = 2;
             if (g.l4_len < 8) { g.st = SMOL_ST_MALFORMED; break; }
             g.span_end = l4 + g.l4_len;
+            if (emit && g.proto == P_ICMP4) {
+                const uint32_t t = rd(l4);
+                if ((t == 3 || t == 11) && g.l4_len >= 28 && (rd(l4 + 8) >> 4) == 4) {
+                    const uint32_t ihl = (rd(l4 + 8) & 0x0fu) * 4;  // Ipv4Packet::header_len, as fill_checksum
+                    if (ihl >= 20 && 8 + ihl <= g.l4_len) {
+                        g.in_off = l4 + 8;
+                        g.in_hl = ihl;
+                    }
+                }
+            }
             break;
-        default:  // P_ICMP6
+        default: {  // P_ICMP6
             g.fo = 2;
-            if (g.l4_len < 4) { g.st = SMOL_ST_MALFORMED; break; }
+            const uint32_t need = (emit || g.l4_len < 4) ? 4u : icmpv6_min_len(rd(l4));
+            if (need == 0 || g.l4_len < need) { g.st = SMOL_ST_MALFORMED; break; }
             g.span_end = l4 + g.l4_len;
             break;
+        }
     }
     return g;
 }

@@ -39,11 +39,9 @@ struct KParams {
     uint16_t* out16;  // MODE_DATA
     uint8_t* status;  // MODE_VERIFY (required), MODE_EMIT (optional)
     const uint8_t* dummy;  // 16-byte-aligned device line read by loads that have nothing to read
-    uint64_t* patch;       // MODE_EMIT two-pass: one meta word per record (csum_walk.h) or nullptr
     uint32_t num_cu;       // compute units of the device (grid sizing)
     const uint8_t* src;             // MODE_COPY: payload source buffer
     const smol_csum_copy_t* copy;   // MODE_COPY: one payload copy per record (16-B aligned)
-    uint8_t* lines;  // MODE_EMIT two-pass, fixed stride: 128-B line slot per record (or nullptr)
     const uint8_t* addrs;  // 6LoWPAN NHC UDP batches: 32 B (IPv6 src, dst) per record, else nullptr
 };
 
@@ -67,7 +65,6 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
 // The same for 6LoWPAN NHC UDP batches (p.addrs set), csum_walk_nhc.hip.
 template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s);
-hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s);
 // Tile kernel (csum_tile.hip), emit / verify only; var 0 = non-temporal loads, 1 = plain loads.
 hipError_t launch_tile(int mode, int shape, int var, int tile_records, const KParams& p, uint32_t max_blocks,
                        hipStream_t s);

@@ -284,11 +284,11 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
                 const uint32_t x = head + o;
                 return x < wvalid ? wbyte(row, x) : ld_byte_sync(my_a0 + o);
             };
-            const Geom g = parse_geometry(rd, my_len, my_kind);
+            const Geom g = parse_geometry(rd, my_len, my_kind, MODE == MODE_EMIT);
             const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
             uint32_t st = g.st;
             uint32_t ip_valid = 1, ip_ok = 1, l4_valid = 1, l4_ok = 1, partial = 0;
-            uint32_t ip_val = 0, l4_val = 0, fpos = 0;
+            uint32_t ip_val = 0, l4_val = 0, fpos = 0, in_val = 0;
             auto rsum = [&](uint32_t from, uint32_t to) -> uint32_t {  // record offsets
                 if (head + to <= wvalid) return region_sum(row, base, head + from, head + to);
                 uint32_t a = 0;  // slow path: straddles or leaves the window
@@ -316,9 +316,17 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
                 // L4 span sum = whole-buffer sum - [aligned start, l4_off) - [span_end, len)
                 uint32_t s = L.sum[lane] - rsum(0, g.l4_off) - (head ? region_sum(row, base, 0, head) : 0u);
                 if (g.span_end < my_len) s -= rsum(g.span_end, my_len);
+                auto word = [&](uint32_t v) { return odd ? v : bswap16(v); };  // BE u16 at an even offset
                 if (MODE == MODE_EMIT) {
-                    const uint32_t f0 = field >> 8, f1 = field & 0xffu;
-                    s -= odd ? ((f0 << 8) + f1) : (f0 + (f1 << 8));
+                    s -= word(field);
+                    if (g.in_off) {  // ICMPv4 error: the embedded IPv4 header first (csum_device.h)
+                        uint32_t hin = 0;
+                        for (uint32_t i = 0; i < g.in_hl / 2; ++i)
+                            if (i != 5) hin += (rd(g.in_off + 2 * i) << 8) | rd(g.in_off + 2 * i + 1);
+                        in_val = caps_tx(p.caps_ipv4) ? (~fold32(hin) & 0xffffu) : 0u;
+                        const uint32_t fi = g.in_off + 10;
+                        s = s - word((rd(fi) << 8) | rd(fi + 1)) + word(in_val);
+                    }
                 }
                 const uint32_t f = fold32(s);
                 const uint32_t dat = odd ? f : bswap16(f);  // == checksum::data(span)
@@ -354,6 +362,7 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
             const uint64_t r = r0 + lane;
             if (MODE == MODE_EMIT) {
                 if (g.fam == 4) store_be16((gu8)(my_a0 + g.ip_off + 10), ip_val);
+                if (g.in_off) store_be16((gu8)(my_a0 + g.in_off + 10), in_val);
                 if (l4) store_be16((gu8)(my_a0 + fpos), l4_val);
                 if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
             } else {

@@ -26,12 +26,9 @@
 // aligned u16 words (v_sad_u16); DPP row reductions combine the group; one lane finishes the
 // record: fold, byte-swap for an odd record start (RFC 1071 §2(B)), pseudo-header, gate, write.
 //
-// Emit writes two 2-byte fields per record.  In place, each is a partial-line write that HBM
-// merges with a read-modify-write, interleaved with the read stream (tools/probe_wr.hip: ~0.1 ms
-// per 2^20 records at 1.5 KB).  The two-pass emit (p.patch != nullptr) instead records one meta
-// word per record and, for fixed-stride batches on the line grid, copies the patched 64-byte
-// line(s) holding the fields from the LDS window to a compact workspace; scatter_kernel then
-// writes whole lines (no HBM read-modify-write) after the read pass.
+// Emit writes two 2-byte fields per record (three for an ICMPv4 error message: the embedded IPv4
+// header's too).  In place, each is a partial-line write that HBM merges with a read-modify-write,
+// interleaved with the read stream (tools/probe_wr.hip: ~0.1 ms per 2^20 records at 1.5 KB).
 //
 // See csum_device.h for the arithmetic and the reference lines each rule follows.
 //
@@ -257,17 +254,6 @@ __device__ __forceinline__ uint32_t sum_masked_words(const u32x4& c, int lo, int
 }
 
 
-// Two-pass emit, meta word per record (p.patch[r]):
-//   bits  0-13 record offset of the IPv4 header-checksum field (MF_NONE: no field), bit 15 MF_LINES
-//   bits 16-29 record offset of the L4 checksum field (MF_NONE: no field)
-//   bits 32-47 / 48-63 the values to write there (host order, stored big-endian).
-// MF_LINES: the 64-B line(s) holding the fields, fields patched in, sit in the record's 128-B
-// workspace slot p.lines + 128 r.  Field offsets are < 0x3fff (at most Ethernet + IPv6 + a
-// 2048-byte Hop-by-Hop header + 16).
-constexpr uint32_t MF_NONE = 0x3fffu;
-constexpr uint32_t MF_LINES = 0x8000u;
-constexpr uint32_t LINE_SLOT = 128;  // workspace bytes per record (two 64-B lines)
-
 // Per-group walk state.
 struct Walk {
     uint64_t r;      // current record
@@ -277,39 +263,21 @@ struct Walk {
     Geom g;          // cur's geometry (protocol modes)
     int s1;          // end of the summed span, relative to the record start
     uint32_t acc, acc2;
-    uint32_t fip, fl4;  // MODE_COPY: record offsets of the fields emit writes (NO_FIELD if none)
+    uint32_t fip, fl4, fin;  // MODE_COPY: record offsets of the fields emit writes (NO_FIELD if none)
 };
 
 constexpr uint32_t NO_FIELD = 0x3fffffffu;
-
-// The 64-B lines a record's emit writes: [l0, l0 + 64 * nl) covering the bytes of both fields.
-// nl == 0 when the fields need more than two consecutive lines.
-struct FieldLines {
-    uint64_t l0;
-    uint32_t nl;
-};
-__device__ __forceinline__ FieldLines field_lines(uint64_t a0, uint32_t fip, uint32_t fl4) {
-    const bool hi4 = fip != MF_NONE, hl4 = fl4 != MF_NONE;
-    const uint64_t lo = a0 + (hi4 && hl4 ? min(fip, fl4) : hi4 ? fip : fl4);
-    const uint64_t hi = a0 + 1 + (hi4 && hl4 ? max(fip, fl4) : hi4 ? fip : fl4);
-    FieldLines f;
-    f.l0 = lo & ~63ull;
-    const uint64_t l1 = hi & ~63ull;
-    f.nl = l1 == f.l0 ? 1u : (l1 == f.l0 + 64 ? 2u : 0u);
-    return f;
-}
+constexpr uint32_t MF_NONE = 0x3fffu;  // no field (finish_gates)
 
 // The gates of one record (MODE_EMIT / MODE_VERIFY / MODE_COPY), run by its whole group once every
 // lane holds its part `acc` of the aligned-word sum over [0, span_end): the header bytes the lanes
 // summed are taken out again, the IPv4 header sum and the pseudo-header address words are read from
 // the LDS window (`winb`, record byte o at head + o), and lane 0 finishes and writes the record.
-template <int G, int MODE, bool IMPLICIT, bool LINE, bool NHC, class RD>
+template <int G, int MODE, bool NHC, class RD>
 __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, uint32_t acc, const RD& rd,
-                                             const uint8_t* winb, uint32_t head, uint64_t a0, uint32_t len,
-                                             uint64_t r, int lane, u32x4* win, uint64_t base, uint32_t* gsh) {
-    constexpr bool COPY = MODE == MODE_COPY;
+                                             const uint8_t* winb, uint32_t head, uint64_t a0, uint64_t r,
+                                             int lane) {
     constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
-    constexpr int WIN = Grid<LINE>::WIN;
     const bool odd = (a0 & 1u) != 0;
     // Header bytes [0, l4_off) that the lanes summed (taken out of the L4 sum), the IPv4
     // header's big-endian word sum and the pseudo-header address words.  All of them sit in
@@ -350,7 +318,7 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
     const gu8 wrec = (gu8)a0;
     if (lane == 0) {
         uint32_t st = g.st;
-        uint32_t fip = MF_NONE, fl4 = MF_NONE, vip = 0, vl4 = 0;  // emit: the field writes
+        uint32_t fip = MF_NONE, fl4 = MF_NONE, fin = MF_NONE, vip = 0, vl4 = 0, vin = 0;  // emit: the field writes
         // IPv4 header: data(header) (canonical fold of the big-endian word sum)
         uint32_t ip_valid = 1, ip_ok = 1;
         if (g.fam == 4) {
@@ -397,11 +365,23 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
             // aligned-word sum of the L4 span = lanes' sum of [0, span_end) minus the
             // header bytes [0, l4_off) (exact: no u32 wrap below 131072 bytes)
             uint32_t s = tot - pre;
+            // aligned-word contribution of a big-endian u16 at an even record offset
+            auto word = [&](uint32_t v) { return odd ? v : bswap16(v); };
             if (EMITS) {
                 // the reference zeroes the field before summing: remove its bytes (the
                 // field offset is even: its parity is the record start's)
-                const uint32_t f0 = field >> 8, f1 = field & 0xffu;
-                s -= odd ? ((f0 << 8) + f1) : (f0 + (f1 << 8));
+                s -= word(field);
+                if (g.in_off) {
+                    // ICMPv4 DstUnreachable / TimeExceeded: Ipv4Repr::emit of the embedded header
+                    // under the same caps (icmpv4.rs:526-528, 540-542; ipv4.rs:605-611) before the
+                    // ICMP checksum covers it.  Rare: lane 0 alone.
+                    uint32_t hin = 0;
+                    for (uint32_t i = 0; i < g.in_hl / 2; ++i)
+                        if (i != 5) hin += (rd(g.in_off + 2 * i) << 8) | rd(g.in_off + 2 * i + 1);
+                    fin = g.in_off + 10;
+                    vin = caps_tx(p.caps_ipv4) ? (~fold32(hin) & 0xffffu) : 0u;
+                    s = s - word((rd(fin) << 8) | rd(fin + 1)) + word(vin);
+                }
             }
             const uint32_t f = fold32(s);
             const uint32_t dat = odd ? f : bswap16(f);  // == checksum::data(span)
@@ -433,33 +413,10 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
             }
         }
         if (EMITS) {
-            if (!COPY && p.patch) {
-                // two-pass emit: the fields are written by scatter_kernel after the read
-                // pass.  Fixed-stride batches on the line grid hand over whole 64-B lines
-                // when they lie in the window, inside the batch buffer and end inside
-                // this record (bytes before the record are the previous record's or the
-                // gap's; scatter_kernel checks the previous record's fields).
-                uint32_t lines = 0;
-                if (IMPLICIT && LINE && p.lines && p.stride >= 256 && (fip != MF_NONE || fl4 != MF_NONE)) {
-                    const FieldLines fl = field_lines(a0, fip, fl4);
-                    const uint64_t lend = fl.l0 + 64ull * fl.nl;
-                    if (fl.nl && fl.l0 >= (uint64_t)p.buf && lend <= a0 + len &&
-                        lend <= base + (uint64_t)WIN) {
-                        uint8_t* wb = reinterpret_cast<uint8_t*>(win);
-                        if (fip != MF_NONE) { wb[head + fip] = (uint8_t)(vip >> 8); wb[head + fip + 1] = (uint8_t)vip; }
-                        if (fl4 != MF_NONE) { wb[head + fl4] = (uint8_t)(vl4 >> 8); wb[head + fl4 + 1] = (uint8_t)vl4; }
-                        lines = (uint32_t)((fl.l0 - base) >> 4) | (fl.nl << 8);
-                    }
-                }
-                *gsh = lines;
-                ((GMEM uint64_t*)p.patch)[r] = (uint64_t)(fip | (lines ? MF_LINES : 0u)) |
-                                               ((uint64_t)fl4 << 16) | ((uint64_t)vip << 32) |
-                                               ((uint64_t)vl4 << 48);
-            } else {
-                if (fip != MF_NONE) store_be16(wrec + fip, vip);
-                if (fl4 != MF_NONE) store_be16(wrec + fl4, vl4);
-                if (NHC && nb0 != NO_FIELD) wrec[0] = (uint8_t)nb0;
-            }
+            if (fip != MF_NONE) store_be16(wrec + fip, vip);
+            if (fin != MF_NONE) store_be16(wrec + fin, vin);
+            if (fl4 != MF_NONE) store_be16(wrec + fl4, vl4);
+            if (NHC && nb0 != NO_FIELD) wrec[0] = (uint8_t)nb0;
             if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
         } else {
             const bool mal = (st & SMOL_ST_MALFORMED) != 0;
@@ -468,15 +425,6 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
                   (l4_valid ? SMOL_ST_L4_VALID : 0u) |
                   ((ip_ok && l4_ok && !mal) ? SMOL_ST_ACCEPT : 0u);
             ((gu8)p.status)[r] = (uint8_t)st;
-        }
-    }
-    if constexpr (MODE == MODE_EMIT && IMPLICIT && LINE) {
-        if (p.patch && p.lines) {  // copy the patched line(s) from the window to the slot
-            wave_lds_sync();
-            const uint32_t lines = *gsh;
-            const uint32_t nc = 4u * (lines >> 8), c0 = lines & 0xffu;
-            for (uint32_t c = (uint32_t)lane; c < nc; c += G)
-                *(GMEM u32x4*)((uint64_t)p.lines + (uint64_t)LINE_SLOT * r + 16u * c) = win[c0 + c];
         }
     }
 }
@@ -509,7 +457,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
-                                          uint32_t* gsh, int gib) {
+                                          int gib) {
     constexpr bool COPY = MODE == MODE_COPY;
     constexpr int WIN = Grid<LINE>::WIN;
     constexpr int WIN_CH = Grid<LINE>::WIN_CH;
@@ -584,27 +532,28 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                 w.g = Geom{};
                 w.g.st = SMOL_ST_MALFORMED;  // copy range does not fit: record left untouched
             } else {
-                w.g = parse_geometry<NHC>(rd, w.cur.len, w.cur.kind, MODE == MODE_EMIT);
+                w.g = parse_geometry<NHC>(rd, w.cur.len, w.cur.kind, MODE == MODE_EMIT || MODE == MODE_COPY);
             }
             // the lanes sum [0, span_end): the header part is subtracted at the end
             w.s1 = (w.g.proto != P_NONE && !(w.g.st & SMOL_ST_MALFORMED)) ? (int)w.g.span_end : 0;
             if (COPY) {
                 w.fip = w.g.fam == 4 ? w.g.ip_off + 10 : NO_FIELD;
                 w.fl4 = (w.g.proto != P_NONE && !(w.g.st & SMOL_ST_MALFORMED)) ? w.g.l4_off + w.g.fo : NO_FIELD;
+                w.fin = w.g.in_off ? w.g.in_off + 10 : NO_FIELD;
             }
         }
     }
     if constexpr (COPY) {  // store the payload bytes of this step (all of them, summed or not)
         const gu8 cbase = (gu8)base;
-        const int f0b = (int)w.fip, f1b = (int)w.fl4;
+        const int f0b = (int)w.fip, f1b = (int)w.fl4, f2b = (int)w.fin;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t k = w.step * (G * U) + u * G + lane;
             const int pos = (int)(16u * k) - (int)head;
             const int lo = (int)w.cur.p0 - pos, hi = (int)w.cur.p1 - pos;
             if (k < w.nch && w.cur.p1 > w.cur.p0 && hi > 0 && lo < 16) {
-                const int f0 = f0b - pos, f1 = f1b - pos;
-                const bool field = (f0 > -2 && f0 < 16) || (f1 > -2 && f1 < 16);
+                const int f0 = f0b - pos, f1 = f1b - pos, f2 = f2b - pos;
+                const bool field = (f0 > -2 && f0 < 16) || (f1 > -2 && f1 < 16) || (f2 > -2 && f2 < 16);
                 const gu8 dst = cbase + 16u * k;
                 if (lo <= 0 && hi >= 16 && !field) {
                     *(GMEM u32x4*)dst = cm[u];
@@ -615,6 +564,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                         uint32_t keep = byte_mask(lo, hi, i);
                         keep &= ~byte_mask(f0, f0 + 2, i);
                         keep &= ~byte_mask(f1, f1 + 2, i);
+                        keep &= ~byte_mask(f2, f2 + 2, i);
                         if (keep == 0xffffffffu) {
                             *(GMEM uint32_t*)(dst + 4 * i) = cw[i];
                         } else if (keep) {
@@ -668,8 +618,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const uint32_t tot = group_sum<G>(s_rel);
             if (lane == 0) ((gu16)p.out16)[r] = (uint16_t)bswap16(fold32(tot));
         } else {
-            finish_gates<G, MODE, IMPLICIT, LINE, NHC>(p, w.g, w.acc, rd, winb, head, w.cur.a0, w.cur.len, r, lane, win,
-                                                  base, gsh);
+            finish_gates<G, MODE, NHC>(p, w.g, w.acc, rd, winb, head, w.cur.a0, r, lane);
         }
     }
 
@@ -700,7 +649,6 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr int GPB = 256 / G;
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     __shared__ u32x4 win[GPB][Grid<LINE>::WIN_CH];
-    __shared__ uint32_t gsh[GPB];
 
     const int lane = (int)(threadIdx.x % G);
     const int gib = (int)(threadIdx.x / G);
@@ -715,7 +663,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     w.g = Geom{};
     w.s1 = 0;
     w.acc = w.acc2 = 0;
-    w.fip = w.fl4 = NO_FIELD;
+    w.fip = w.fl4 = w.fin = NO_FIELD;
 
     Regs<U, COPY> va;
     if (PF) {
@@ -724,60 +672,14 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
                                             shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU>(p, w, va, vb, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU>(p, w, vb, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU>(p, w, va, vb, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU>(p, w, vb, va, lane, ngroups, &win[gib][0], gib)) break;
         }
     } else {
         while (true) {
             load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
                                             shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC>(p, w, va, va, lane, ngroups, &win[gib][0], &gsh[gib], gib)) break;
-        }
-    }
-}
-
-// Second pass of the two-pass emit: 8 lanes per record apply its meta word.  MF_LINES records
-// write their whole 64-B line(s) from the workspace slot — unless a field of the previous record
-// lies inside them (its bytes in the slot are the pre-emit ones), then, like every other record,
-// they store the two 2-byte fields.  A record's lines end inside the record and start at most
-// 63 bytes before it, and records are >= 256 bytes apart, so only the previous record can meet
-// them, and only it can have a field there.
-template <bool IMPLICIT>
-__global__ __launch_bounds__(256) void scatter_kernel(KParams p) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < 8 * p.n; t += stride) {
-        const uint64_t r = t >> 3;
-        const uint32_t c = (uint32_t)(t & 7u);
-        const uint64_t m = ((const GMEM uint64_t*)p.patch)[r];
-        const uint32_t fip = (uint32_t)m & MF_NONE, fl4 = (uint32_t)(m >> 16) & MF_NONE;
-        const uint32_t vip = (uint32_t)(m >> 32) & 0xffffu, vl4 = (uint32_t)(m >> 48);
-        if (fip == MF_NONE && fl4 == MF_NONE) continue;
-        uint64_t a0;
-        if (IMPLICIT) {
-            a0 = (uint64_t)p.buf + r * p.stride;
-        } else {
-            const GMEM uint64_t* d = (const GMEM uint64_t*)((uint64_t)p.desc + 16 * r);
-            a0 = (uint64_t)p.buf + d[0];
-        }
-        bool as_lines = IMPLICIT && (m & MF_LINES);
-        FieldLines fl = {0, 0};
-        if (as_lines) {
-            fl = field_lines(a0, fip, fl4);
-            if (r > 0) {
-                const uint64_t mp = ((const GMEM uint64_t*)p.patch)[r - 1];
-                const uint64_t ap = a0 - p.stride;
-                const uint64_t lend = fl.l0 + 64ull * fl.nl;
-                const uint32_t pf[2] = {(uint32_t)mp & MF_NONE, (uint32_t)(mp >> 16) & MF_NONE};
-                for (int i = 0; i < 2; ++i)
-                    if (pf[i] != MF_NONE && ap + pf[i] + 2 > fl.l0 && ap + pf[i] < lend) as_lines = false;
-            }
-        }
-        if (as_lines) {
-            if (c < 4 * fl.nl)
-                *(GMEM u32x4*)(fl.l0 + 16u * c) = *(const GMEM u32x4*)((uint64_t)p.lines + (uint64_t)LINE_SLOT * r + 16u * c);
-        } else if (c == 0) {
-            if (fip != MF_NONE) store_be16((gu8)(a0 + fip), vip);
-            if (fl4 != MF_NONE) store_be16((gu8)(a0 + fl4), vl4);
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC>(p, w, va, va, lane, ngroups, &win[gib][0], gib)) break;
         }
     }
 }

@@ -1,16 +1,8 @@
-// Instantiates the fused copy + emit walk kernel and the two-pass emit's scatter pass
-// (csum_walk.h), and dispatches a batched call to its instantiation.
+// Instantiates the fused copy + emit walk kernel (csum_walk.h), and dispatches a batched call to its
+// instantiation.
 #include "csum_walk.h"
 
 namespace smolcsum {
-
-hipError_t launch_scatter(const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    const uint64_t want = (8 * p.n + 255) / 256;
-    const uint32_t blocks = grid_blocks(want, max_blocks);
-    if (p.desc) hipLaunchKernelGGL(scatter_kernel<false>, dim3(blocks), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(scatter_kernel<true>, dim3(blocks), dim3(256), 0, s, p);
-    return hipGetLastError();
-}
 
 hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const bool implicit = p.desc == nullptr;

@@ -242,14 +242,6 @@ class ChecksumEngine:
     def set_variant(self, variant: int):
         check(lib().smol_csum_tool_set_variant(self._h, int(variant)), "smol_csum_tool_set_variant")
 
-    def set_deferred_emit(self, mode):
-        """Emit strategy: True / 1 two passes, False / 0 stores in the read pass, None / -1 auto."""
-        m = -1 if mode is None else int(mode)
-        check(lib().smol_csum_tool_set_deferred_emit(self._h, m), "smol_csum_tool_set_deferred_emit")
-
-    def reserve(self, max_records: int):
-        check(lib().smol_csum_ctx_reserve(self._h, int(max_records)), "smol_csum_ctx_reserve")
-
     def set_tile(self, records: int):
         check(lib().smol_csum_tool_set_tile(self._h, int(records)), "smol_csum_tool_set_tile")
 

@@ -231,7 +231,6 @@ public:
         check(smol_csum_batch_data(ctx_, d_buf, &bc, d_out, stream), "smol_csum_batch_data");
     }
 
-    void reserve(uint64_t max_records) { check(smol_csum_ctx_reserve(ctx_, max_records), "smol_csum_ctx_reserve"); }
 
     smol_csum_ctx_t* handle() const { return ctx_; }
 

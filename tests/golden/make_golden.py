@@ -129,6 +129,42 @@ def pretty_print_example():
     }]
 
 
+def icmpv6_check_len():
+    """The message-type length rule of Icmpv6Packet::check_len (src/wire/icmpv6.rs), read from the
+    source text: the Message enum values, the field ranges, header_len()'s match arms and the list
+    of types check_len holds to ``len >= HEADER_END && len >= header_len()``.  Returns the minimum
+    length per type value (0 = check_len rejects the type under the default feature set)."""
+    rel = "src/wire/icmpv6.rs"
+    text = _read(rel)
+    enum = re.search(r"pub enum Message\(u8\)\s*\{(.*?)\}", text, re.S).group(1)
+    values = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"(\w+)\s*=\s*(0x[0-9a-fA-F]+)", enum)}
+    fields = {}
+    for m in re.finditer(r"pub const (\w+): (Field|usize) = ([^;]+);", text):
+        v = m.group(3).strip()
+        if m.group(2) == "Field":
+            a, b = v.split("..")
+            fields[m.group(1)] = int(eval(b, {}, {}))  # "end" of a literal range such as 8..8 + 16
+        else:
+            fields[m.group(1)] = int(v, 0)
+    hl = re.search(r"pub fn header_len\(&self\) -> usize \{(.*?)\n    \}", text, re.S)
+    header_len = {m.group(1): fields[m.group(2)]
+                  for m in re.finditer(r"Message::(\w+) => field::(\w+)\.end", hl.group(1))}
+    default_len = fields["CHECKSUM"]
+    cl = re.search(r"pub fn check_len\(&self\) -> Result<\(\)> \{(.*?)\n    \}", text, re.S)
+    arm = re.search(r"match self\.msg_type\(\) \{\s*((?:\|?\s*Message::\w+\s*)+)=>\s*\{\s*if len < field::HEADER_END "
+                    r"\|\| len < self\.header_len\(\)", cl.group(1), re.S)
+    listed = re.findall(r"Message::(\w+)", arm.group(1))
+    line = text[: cl.start()].count("\n") + 1
+    table = {}
+    for name, val in sorted(values.items(), key=lambda kv: kv[1]):
+        if name in listed:
+            table[val] = max(fields["HEADER_END"], header_len.get(name, default_len))
+        else:
+            table[val] = 0  # RplControl: only with feature proto-rpl (not in Cargo.toml's default)
+    return {"min_len": {str(k): v for k, v in table.items()}, "names": {str(v): k for k, v in values.items()},
+            "generic_min": 4, "cite": f"{rel}:{line} check_len, header_len, mod field; Cargo.toml default features"}
+
+
 def main():
     kats = []
 
@@ -201,6 +237,7 @@ def main():
 
     nhc = sixlowpan_nhc_udp()
     pretty = pretty_print_example()
+    icmp6 = icmpv6_check_len()
 
     doc = {
         "generator": "tests/golden/make_golden.py",
@@ -210,6 +247,7 @@ def main():
         "fuzz_corpus_frames": corpus,
         "sixlowpan_nhc_udp": nhc,
         "pretty_print": pretty,
+        "icmpv6_check_len": icmp6,
     }
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)

@@ -55,6 +55,17 @@ def icmp_echo(t: int, payload: bytes, csum: int = 0) -> bytes:
     return bytes([t, 0]) + be16(csum) + be16(0x1234) + be16(0xABCD) + payload
 
 
+def icmp4_error(t: int, code: int, inner: bytes, csum: int = 0) -> bytes:
+    """ICMPv4 DstUnreachable (3) / TimeExceeded (11) with `inner` (an IPv4 header + data) after the
+    4 unused bytes, as Icmpv4Repr::emit lays it out (icmpv4.rs:520-543)."""
+    return bytes([t, code]) + be16(csum) + bytes(4) + inner
+
+
+def icmp6(t: int, body_len: int, rng, csum: int = 0) -> bytes:
+    """ICMPv6 message of type t: 4-byte header + body_len random bytes (the check_len tests)."""
+    return bytes([t, 0]) + be16(csum) + rand_bytes(rng, body_len)
+
+
 def eth(payload: bytes, ethertype: int = 0x0800) -> bytes:
     return bytes([0x02, 0, 0, 0, 0, 1, 0x02, 0, 0, 0, 0, 2]) + be16(ethertype) + payload
 

@@ -444,16 +444,15 @@ def test_grid_cap_huge_batch(eng):
     assert int((st == int(ref)).sum()) == n and (ref & E.ST_ACCEPT)
 
 
-def _emit_case(eng, host, off, n, stride, L, kind, caps, variant, defer, shape=-1, blocks=0):
+def _emit_case(eng, host, off, n, stride, L, kind, caps, variant, shape=-1, blocks=0):
     """Emit a fixed-stride batch that starts `off` bytes into `host` (a device copy of it) and
     compare the WHOLE buffer with the oracle: bytes outside the records (before the batch, gaps,
-    neighbours rewritten by whole-line writes) must not change."""
+    neighbours' lines) must not change."""
     full = torch.from_numpy(host.copy()).cuda()
     d = full[off:]
     batch = E.Batch.fixed(n, stride, L, kind)
     st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
     eng.set_variant(variant)
-    eng.set_deferred_emit(defer)
     eng.set_shape(shape)
     eng.set_max_blocks(blocks)
     try:
@@ -461,7 +460,6 @@ def _emit_case(eng, host, off, n, stride, L, kind, caps, variant, defer, shape=-
         got = full.cpu().numpy()
     finally:
         eng.set_variant(-1)
-        eng.set_deferred_emit(None)
         eng.set_shape(-1)
         eng.set_max_blocks(0)
     ref = host.copy()
@@ -469,17 +467,17 @@ def _emit_case(eng, host, off, n, stride, L, kind, caps, variant, defer, shape=-
     ref_st = oracle.batch_emit(sub, None, n, stride, L, kind, caps)
     ref[off:] = sub
     diff = np.nonzero(got != ref)[0]
-    assert diff.size == 0, (stride, L, off, variant, defer, shape, blocks, caps, diff[:8])
-    assert np.array_equal(st.cpu().numpy(), ref_st), (stride, L, off, variant, defer)
+    assert diff.size == 0, (stride, L, off, variant, shape, blocks, caps, diff[:8])
+    assert np.array_equal(st.cpu().numpy(), ref_st), (stride, L, off, variant)
 
 
 @pytest.mark.parametrize("profile,kind", [(E.SYNTH_UDP4, E.KIND_IP), (E.SYNTH_TCP4, E.KIND_IP),
                                           (E.SYNTH_V6MIX, E.KIND_IP), (E.SYNTH_ETH_TCP4, E.KIND_ETH)])
-def test_emit_two_pass_match_oracle(eng, profile, kind):
-    """Fixed-stride emit in every strategy (two-pass with whole-line writes — the default on the
-    line grid — two-pass with 2-byte stores only, stores in the read pass) against the oracle over
-    the whole buffer: strides below / at / above the 256-byte line-write threshold, odd strides and
-    odd batch starts, gaps (stride > len), every shape, persistent grids, caps that write zeros."""
+def test_emit_variants_match_oracle(eng, profile, kind):
+    """Fixed-stride emit in every kernel variant (line grid with shared boundary lines — the
+    default — cached field lines, 16-byte grid, cached / non-temporal loads) against the oracle
+    over the whole buffer: short, odd and line-sized strides, odd batch starts, gaps (stride > len),
+    every shape, persistent grids, caps that write zeros."""
     rng = np.random.default_rng(profile)
     for stride, L in [(64, 64), (97, 97), (200, 200), (255, 255), (256, 256), (257, 257), (300, 256),
                       (1500, 1500), (1501, 1501), (1519, 1500), (4000, 4000)]:
@@ -489,19 +487,18 @@ def test_emit_two_pass_match_oracle(eng, profile, kind):
             tmp = torch.from_numpy(host[off:].copy()).cuda()
             eng.synth(tmp, E.Batch.fixed(n, stride, L, kind), profile, seed=stride * 13 + profile + off)
             host[off:] = tmp.cpu().numpy()
-            for variant, defer, shape, blocks, caps in [
-                    (-1, None, -1, 0, (0, 0, 0, 0, 0)), (5, 1, 0, 3, (0, 0, 0, 0, 0)),
-                    (6, 1, 1, 0, (2, 3, 0, 1, 0)), (5, 1, 7, 0, (0, 0, 0, 0, 0)),
-                    (5, 1, 8, 5, (3, 2, 2, 3, 3)), (5, 0, 5, 0, (0, 0, 0, 0, 0)),
-                    (1, 1, 3, 0, (0, 0, 0, 0, 0)), (1, 0, 0, 0, (0, 0, 0, 0, 0))]:
-                _emit_case(eng, host, off, n, stride, L, kind, caps, variant, defer, shape, blocks)
+            for variant, shape, blocks, caps in [
+                    (-1, -1, 0, (0, 0, 0, 0, 0)), (5, 0, 3, (0, 0, 0, 0, 0)),
+                    (6, 1, 0, (2, 3, 0, 1, 0)), (5, 7, 0, (0, 0, 0, 0, 0)),
+                    (5, 8, 5, (3, 2, 2, 3, 3)), (9, 5, 0, (0, 0, 0, 0, 0)),
+                    (10, 7, 0, (0, 0, 0, 0, 0)), (1, 3, 0, (0, 0, 0, 0, 0)), (0, 0, 0, (0, 0, 0, 0, 0))]:
+                _emit_case(eng, host, off, n, stride, L, kind, caps, variant, shape, blocks)
 
 
-def test_emit_two_pass_neighbour_fields(eng):
-    """Whole-line field writes reach up to 63 bytes into the previous record.  Records whose L4
-    checksum field sits in their last 64 bytes (IPv6 Hop-by-Hop pushes it there) alternate with
-    IPv4 / IPv6 records whose field lines start before them: the scatter pass must fall back to
-    2-byte stores wherever a line would carry the previous record's stale field."""
+def test_emit_neighbour_fields(eng):
+    """Records whose L4 checksum field sits in their last 64 bytes (IPv6 Hop-by-Hop pushes it
+    there, into the boundary line the next record's group loads) alternate with IPv4 / IPv6
+    records whose field lines start in the previous record's last line."""
     rng = np.random.default_rng(77)
     a6, b6 = bytes(range(16)), bytes(range(16, 32))
     for stride in (256, 257, 300, 301, 320):
@@ -522,13 +519,13 @@ def test_emit_two_pass_neighbour_fields(eng):
         for off in (0, 5, 40, 63):
             host = np.concatenate([rng.integers(0, 256, off, dtype=np.uint8),
                                    np.frombuffer(b"".join(recs), np.uint8), np.zeros(128, np.uint8)])
-            for variant, defer in [(-1, None), (5, 1), (6, 1), (1, 1), (0, 0), (5, 0)]:
-                _emit_case(eng, host, off, n, stride, stride, E.KIND_IP, CAPS_DEFAULT, variant, defer)
+            for variant in (-1, 5, 6, 1, 0, 9):
+                _emit_case(eng, host, off, n, stride, stride, E.KIND_IP, CAPS_DEFAULT, variant)
 
 
-def test_emit_two_pass_chunks(eng):
-    """More records than one two-pass workspace chunk (2^20): chunk boundaries, and the first
-    record of each chunk (it cannot see the previous chunk's meta words)."""
+def test_emit_large_batch(eng):
+    """More than 2^20 records at short strides (256 / 257 B: many records per group's line
+    window neighbourhood), the whole buffer against the oracle."""
     n, L = (1 << 20) + 37, 256
     for stride, off in ((256, 0), (257, 11)):
         host = np.zeros(off + n * stride + 128, dtype=np.uint8)
@@ -536,7 +533,7 @@ def test_emit_two_pass_chunks(eng):
         eng.synth(tmp, E.Batch.fixed(n, stride, L, E.KIND_IP), E.SYNTH_UDP4, seed=stride)
         host[off:] = tmp.cpu().numpy()
         del tmp
-        _emit_case(eng, host, off, n, stride, L, E.KIND_IP, CAPS_DEFAULT, -1, None)
+        _emit_case(eng, host, off, n, stride, L, E.KIND_IP, CAPS_DEFAULT, -1)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])

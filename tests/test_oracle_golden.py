@@ -237,3 +237,60 @@ def test_pseudo_header_v4_v6():
             pyref.pseudo_header_v6(s6.tobytes(), d6.tobytes(), proto, ln)
     with pytest.raises(ValueError):
         pyref.pseudo_header(b"\x00" * 4, b"\x00" * 16, 6, 0)
+
+
+def test_icmpv6_check_len_table(golden):
+    """oracle_icmpv6_min_len restates Icmpv6Packet::check_len's per-type rule: pinned to the table
+    make_golden.py extracted from src/wire/icmpv6.rs (enum values, field ends, header_len arms,
+    the check_len arm) for every type value; types the enum does not name are Message::Unknown."""
+    tab = golden["icmpv6_check_len"]["min_len"]
+    L = oracle.lib()
+    for t in range(256):
+        assert L.oracle_icmpv6_min_len(t) == tab.get(str(t), 0), t
+
+
+def test_icmpv6_truncated_typed_messages_malformed(golden):
+    """A typed ICMPv6 message shorter than its header is dropped by check_len before the
+    checksum gate (SMOL_ST_MALFORMED, no ACCEPT) even with a correct checksum; at its minimum
+    length it passes.  Emit keeps the generic len >= 4 rule (fill_checksum covers any type)."""
+    from tests import pktgen as P
+
+    rng = np.random.default_rng(6)
+    a6, b6 = bytes(range(16)), bytes(range(16, 32))
+    tab = {int(k): v for k, v in golden["icmpv6_check_len"]["min_len"].items()}
+    for t in list(range(256)):
+        need = tab.get(t, 0)
+        for body in sorted({0, 3, 4, max(need - 5, 0), max(need - 4, 0), need, need + 3}):
+            msg = P.icmp6(t, body, rng)
+            rec = np.frombuffer(P.ipv6(a6, b6, 58, msg), np.uint8).copy()
+            oracle.batch_emit(rec, None, 1, len(rec), len(rec), 1)  # fill (generic rule)
+            st = int(oracle.batch_verify(rec, None, 1, len(rec), len(rec), 1)[0])
+            ok = need != 0 and len(msg) >= need
+            assert bool(st & ST_MALFORMED) == (not ok), (t, len(msg), st)
+            assert bool(st & ST_ACCEPT) == ok, (t, len(msg), st)
+            assert pyref.icmpv6_verify(bytes(rec[40:]), a6, b6)  # the fill itself is valid
+
+
+def test_icmpv4_error_embedded_header_corpus(golden):
+    """fuzz/corpus/packet_parser/icmpv4_unreachable.bin is a real DstUnreachable message whose
+    embedded IPv4 header checksum (0xb0b4), ICMP checksum and outer header checksum were written by
+    its sender.  Zero all three (what the stack writes under offloaded caps), emit with default
+    caps: the frame must come back byte for byte.  With caps.ipv4 = None the inner (and outer)
+    header field stays 0 and the ICMP checksum covers that."""
+    fr = [f for f in golden["fuzz_corpus_frames"] if f["name"] == "icmpv4_unreachable.bin"][0]
+    orig = _arr(bytes.fromhex(fr["bytes"]))
+    ip = 14
+    hl = (orig[ip] & 15) * 4
+    icmp = ip + hl
+    assert orig[icmp] == 3 and orig[icmp + 8] >> 4 == 4
+    z = orig.copy()
+    for off in (ip + 10, icmp + 2, icmp + 8 + 10):
+        z[off:off + 2] = 0
+    got = z.copy()
+    st = oracle.batch_emit(got, None, 1, got.size, got.size, 2)
+    assert st[0] == 0 and np.array_equal(got, orig)
+    got = z.copy()
+    oracle.batch_emit(got, None, 1, got.size, got.size, 2, caps=(3, 0, 0, 0, 0))
+    assert got[icmp + 18] == 0 and got[icmp + 19] == 0 and got[ip + 10] == 0
+    tot = int.from_bytes(bytes(orig[ip + 2:ip + 4]), "big")
+    assert pyref.icmpv4_verify(bytes(got[icmp:ip + tot]))

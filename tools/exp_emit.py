@@ -41,9 +41,6 @@ def main():
         t("emit(tx) caps=ignored", lambda: eng.emit(wl.tx, wl.batch, caps=(3, 3, 3, 3, 3), stream=s))
         t("emit(tx)+verify(rx)", lambda: (eng.emit(wl.tx, wl.batch, stream=s), eng.verify(wl.rx, wl.batch, status=st, stream=s)))
         t("verify(tx)+verify(rx)", lambda: (eng.verify(wl.tx, wl.batch, status=st, stream=s), eng.verify(wl.rx, wl.batch, status=st, stream=s)))
-        eng.set_deferred_emit(False)
-        t("emit(tx) direct stores", lambda: eng.emit(wl.tx, wl.batch, stream=s))
-        eng.set_deferred_emit(True)
         sink = torch.zeros(1, dtype=torch.int32, device=dev)
         t("stream_read(tx)", lambda: eng.stream_read(wl.tx, sink, stream=s))
 

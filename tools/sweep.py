@@ -26,7 +26,6 @@ def main():
     ap.add_argument("--shapes", default="0,1,2,3,4,5,6,7,8")
     ap.add_argument("--blocks", default="0")
     ap.add_argument("--var", default="0,1,2")
-    ap.add_argument("--defer", default="-1", help="emit strategy: -1 auto, 0 in-pass stores, 1 two-pass")
     ap.add_argument("--tile", default="32")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -38,12 +37,10 @@ def main():
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     for rnd in range(2):
         for shape in [int(x) for x in args.shapes.split(",")]:
-            for var, bpc, defer, tile in [(a, b, c, d) for a in [int(x) for x in args.var.split(",")]
-                                          for b in [int(x) for x in args.blocks.split(",")]
-                                          for c in [int(x) for x in args.defer.split(",")]
-                                          for d in [int(x) for x in args.tile.split(",")]]:
+            for var, bpc, tile in [(a, b, d) for a in [int(x) for x in args.var.split(",")]
+                                   for b in [int(x) for x in args.blocks.split(",")]
+                                   for d in [int(x) for x in args.tile.split(",")]]:
                 if True:
-                    eng.set_deferred_emit(defer)
                     eng.set_shape(shape)
                     eng.set_variant(var)
                     eng.set_tile(tile)
@@ -62,7 +59,7 @@ def main():
                     torch.cuda.synchronize()
                     em = ev[0].elapsed_time(ev[1]) / args.reps
                     vm = ev[1].elapsed_time(ev[2]) / args.reps
-                    row = {"round": rnd, "shape": shape, "var": var, "blocks_per_cu": bpc, "defer": defer, "tile": tile,
+                    row = {"round": rnd, "shape": shape, "var": var, "blocks_per_cu": bpc, "tile": tile,
                            "emit_ms": round(em, 4), "verify_ms": round(vm, 4),
                            "emit_GBs": round(wl.read_bytes / em / 1e6, 1),
                            "verify_GBs": round(wl.read_bytes / vm / 1e6, 1)}
