@@ -205,7 +205,49 @@ int smol_csum_batch_copy_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_c
                               const uint8_t* d_src, const smol_csum_copy_t* d_copy,
                               const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
 
-/* ---- 3. 6LoWPAN next-header-compressed UDP (RFC 6282 §4.3) ------------------------------- */
+/* ---- 3. IPv4 fragment groups ------------------------------------------------------------- */
+
+/* One IPv4 datagram carried by `count` consecutive records of a batch, starting at record
+ * `first` (16 bytes, device memory): its fragments, in any order.  A group of one unfragmented
+ * packet is allowed.  Groups must not share records. */
+typedef struct {
+    uint64_t first;
+    uint32_t count;    /* 1 .. SMOL_MAX_FRAGMENTS */
+    uint32_t reserved; /* must be 0 */
+} smol_csum_frag_group_t;
+
+/* Fragments per group the kernels accept (smoltcp's default fragmentation and reassembly buffers
+ * hold 1500 bytes, gen_config.py; 256 fragments of 8 bytes cover 2 KB, of 1480 bytes 370 KB). */
+#define SMOL_MAX_FRAGMENTS 256u
+
+/* Emit for IPv4 datagrams the stack fragmented under offloaded checksums.  The iface emits the
+ * whole datagram with the device's caps (the L4 checksum written 0) and only then cuts it into
+ * fragments that reach TxToken::consume one by one (src/iface/interface/mod.rs:1276-1331,
+ * src/iface/interface/ipv4.rs:440-490), so the device, holding a datagram's fragments until the
+ * last one, fills per group: every fragment's IPv4 header checksum (caps.ipv4, as
+ * dispatch_ipv4_frag does) and the datagram's L4 checksum — computed over the reassembled payload
+ * exactly as Repr::emit does on the whole datagram, ICMPv4 error messages' embedded header
+ * included — written into the fragment that holds the field.  The result is bit-identical to
+ * "emit the whole datagram, then fragment it".  A group is usable when every record is an IPv4
+ * packet (Medium::Ip, or Ethernet with ethertype 0x0800) passing Ipv4Packet::check_len, all share
+ * the reassembly key (ident, source, destination, protocol: ipv4.rs get_key), the payloads cover
+ * [0, T) exactly once with exactly one last fragment (MF clear) ending at T; otherwise its records
+ * are reported SMOL_ST_MALFORMED and only their own headers are filled.  `d_status` (nullable)
+ * receives SMOL_ST_MALFORMED / SMOL_ST_UNSUPPORTED per record of every group. */
+int smol_csum_batch_emit_frag(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
+                              const smol_csum_frag_group_t* d_groups, uint64_t n_groups,
+                              const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
+
+/* Verify for fragmented IPv4 datagrams (src/iface/interface/ipv4.rs:103-146: every fragment
+ * passes Ipv4Repr::parse, then the reassembled payload reaches the L4 gate).  Per record: its own
+ * IPv4 bits, the datagram's L4 bits, and SMOL_ST_ACCEPT only when every fragment of the group
+ * passes its IPv4 gate and the datagram its L4 gate (a dropped fragment never completes the
+ * datagram).  Records outside every group are not written. */
+int smol_csum_batch_verify_frag(smol_csum_ctx_t* ctx, const uint8_t* d_buf, const smol_csum_batch_t* batch,
+                                const smol_csum_frag_group_t* d_groups, uint64_t n_groups,
+                                const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
+
+/* ---- 4. 6LoWPAN next-header-compressed UDP (RFC 6282 §4.3) ------------------------------- */
 
 /* The IPv6 source and destination addresses of one record (32 bytes, device memory): 6LoWPAN's
  * IPHC header compresses them (to nothing, when they derive from the link-layer addresses), so the

@@ -137,6 +137,11 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.oracle_nhc_udp_verify.restype = ctypes.c_uint8
     L.oracle_nhc_udp_emit.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.POINTER(CapsC)]
     L.oracle_nhc_udp_emit.restype = ctypes.c_uint8
+    for name in ("oracle_batch_emit_frag", "oracle_batch_verify_frag"):
+        f = getattr(L, name)
+        f.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint8, u8p,
+                      ctypes.c_uint64, ctypes.POINTER(CapsC), u8p]
+        f.restype = None
     for name in ("oracle_batch_nhc_udp_emit", "oracle_batch_nhc_udp_verify"):
         f = getattr(L, name)
         f.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, u8p,
@@ -201,6 +206,32 @@ def batch_verify(buf: np.ndarray, desc, n: int, stride: int = 0, length: int = 0
     c = caps_c(caps)
     lib().oracle_batch_verify(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride,
                               length, kind, ctypes.byref(c), _ptr(st))
+    return st
+
+
+FRAG_GROUP_DTYPE = np.dtype([("first", "<u8"), ("count", "<u4"), ("reserved", "<u4")])
+
+
+def batch_emit_frag(buf: np.ndarray, desc, n: int, groups: np.ndarray, stride: int = 0, length: int = 0,
+                    kind: int = 1, caps=(0, 0, 0, 0, 0)):
+    """IPv4 fragment groups, emit (see csum_oracle.c): in place on ``buf``; returns the status
+    array (records outside the groups: 0)."""
+    st = np.zeros(n, dtype=np.uint8)
+    c = caps_c(caps)
+    g = np.ascontiguousarray(groups, dtype=FRAG_GROUP_DTYPE)
+    lib().oracle_batch_emit_frag(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride, length, kind,
+                                 _ptr(g) if g.size else None, g.size, ctypes.byref(c), _ptr(st))
+    return st
+
+
+def batch_verify_frag(buf: np.ndarray, desc, n: int, groups: np.ndarray, stride: int = 0, length: int = 0,
+                      kind: int = 1, caps=(0, 0, 0, 0, 0)):
+    """IPv4 fragment groups, verify; returns the status array (records outside the groups: 0)."""
+    st = np.zeros(n, dtype=np.uint8)
+    c = caps_c(caps)
+    g = np.ascontiguousarray(groups, dtype=FRAG_GROUP_DTYPE)
+    lib().oracle_batch_verify_frag(_ptr(buf), _ptr(desc) if desc is not None else None, n, stride, length, kind,
+                                   _ptr(g) if g.size else None, g.size, ctypes.byref(c), _ptr(st))
     return st
 
 

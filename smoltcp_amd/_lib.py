@@ -27,7 +27,8 @@ ABI_SYMBOLS = [
     "smol_csum_data", "smol_csum_combine", "smol_csum_pseudo_header_v4",
     "smol_csum_pseudo_header_v6", "smol_csum_pseudo_header", "smol_csum_ctx_create",
     "smol_csum_ctx_destroy", "smol_csum_batch_data", "smol_csum_batch_emit",
-    "smol_csum_batch_verify", "smol_csum_batch_copy_emit", "smol_csum_batch_nhc_udp_emit",
+    "smol_csum_batch_verify", "smol_csum_batch_copy_emit", "smol_csum_batch_emit_frag",
+    "smol_csum_batch_verify_frag", "smol_csum_batch_nhc_udp_emit",
     "smol_csum_batch_nhc_udp_verify", "smol_csum_last_error", "smol_csum_abi_version",
 ]
 TOOL_SYMBOLS = [
@@ -108,6 +109,10 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_batch_verify.restype = i32
     L.smol_csum_batch_copy_emit.argtypes = [vp, vp, ctypes.POINTER(BatchC), vp, vp, ctypes.POINTER(Caps), vp, vp]
     L.smol_csum_batch_copy_emit.restype = i32
+    for name in ("smol_csum_batch_emit_frag", "smol_csum_batch_verify_frag"):
+        f = getattr(L, name)
+        f.argtypes = [vp, vp, ctypes.POINTER(BatchC), vp, u64, ctypes.POINTER(Caps), vp, vp]
+        f.restype = i32
     for name in ("smol_csum_batch_nhc_udp_emit", "smol_csum_batch_nhc_udp_verify"):
         f = getattr(L, name)
         f.argtypes = [vp, vp, ctypes.POINTER(BatchC), vp, ctypes.POINTER(Caps), vp, vp]

@@ -261,6 +261,50 @@ int smol_csum_batch_copy_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_c
     return run(ctx, MODE_COPY, d_buf, b, caps, nullptr, d_status, stream, d_src, d_copy);
 }
 
+// ---- IPv4 fragment groups ---------------------------------------------------------------------
+
+static int run_frag(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t* b,
+                    const smol_csum_frag_group_t* d_groups, uint64_t n_groups, const smol_checksum_caps_t* caps,
+                    uint8_t* d_status, void* stream) {
+    if (!ctx || !caps_valid(caps)) return SMOL_EINVAL;
+    int rc = check_batch(b, d_buf);
+    if (rc != SMOL_OK) return rc;
+    if (n_groups == 0) return SMOL_OK;
+    if (b->n == 0 || !d_groups || ((uintptr_t)d_groups & 15u) != 0) return SMOL_EINVAL;
+    if (mode == MODE_VERIFY && !d_status) return SMOL_EINVAL;
+    KParams p;
+    std::memset(&p, 0, sizeof p);
+    p.buf = d_buf;
+    p.desc = b->desc;
+    p.n = b->n;
+    p.stride = b->stride;
+    p.len = b->len;
+    p.kind = b->kind;
+    p.caps_ipv4 = caps->ipv4;
+    p.caps_udp = caps->udp;
+    p.caps_tcp = caps->tcp;
+    p.caps_icmpv4 = caps->icmpv4;
+    p.caps_icmpv6 = caps->icmpv6;
+    p.status = d_status;
+    p.dummy = ctx->dummy;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    hipError_t e = launch_frag(mode, p, d_groups, n_groups, (hipStream_t)stream);
+    return e == hipSuccess ? SMOL_OK : hip_fail(e, "fragment kernel launch");
+}
+
+int smol_csum_batch_emit_frag(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* b,
+                              const smol_csum_frag_group_t* d_groups, uint64_t n_groups,
+                              const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream) {
+    return run_frag(ctx, MODE_EMIT, d_buf, b, d_groups, n_groups, caps, d_status, stream);
+}
+
+int smol_csum_batch_verify_frag(smol_csum_ctx_t* ctx, const uint8_t* d_buf, const smol_csum_batch_t* b,
+                                const smol_csum_frag_group_t* d_groups, uint64_t n_groups,
+                                const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream) {
+    return run_frag(ctx, MODE_VERIFY, const_cast<uint8_t*>(d_buf), b, d_groups, n_groups, caps, d_status, stream);
+}
+
 // ---- 6LoWPAN NHC UDP --------------------------------------------------------------------------
 
 int smol_csum_batch_nhc_udp_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* b,

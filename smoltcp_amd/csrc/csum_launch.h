@@ -81,6 +81,9 @@ struct SynthParams {
 };
 hipError_t launch_synth(const SynthParams& p, uint32_t max_blocks, hipStream_t s);
 hipError_t launch_corrupt(const SynthParams& p, uint32_t every, hipStream_t s);
+// IPv4 fragment groups (csum_frag.hip): MODE_EMIT / MODE_VERIFY, one wavefront per group.
+hipError_t launch_frag(int mode, const KParams& p, const smol_csum_frag_group_t* groups, uint64_t ngroups,
+                       hipStream_t s);
 hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t max_blocks,
                               hipStream_t s);
 

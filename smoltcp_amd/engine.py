@@ -41,6 +41,20 @@ COPY_DTYPE = np.dtype([("src_offset", "<u8"), ("dst_offset", "<u4"), ("len", "<u
 assert COPY_DTYPE.itemsize == 16
 
 
+# smol_csum_frag_group_t: one IPv4 datagram = `count` consecutive records from `first`
+FRAG_GROUP_DTYPE = np.dtype([("first", "<u8"), ("count", "<u4"), ("reserved", "<u4")])
+assert FRAG_GROUP_DTYPE.itemsize == 16
+MAX_FRAGMENTS = 256
+
+
+def make_groups(firsts, counts) -> np.ndarray:
+    """Host array of smol_csum_frag_group_t (view it as uint8 and copy it to the device)."""
+    g = np.zeros(len(firsts), dtype=FRAG_GROUP_DTYPE)
+    g["first"] = np.asarray(firsts, dtype=np.uint64)
+    g["count"] = np.asarray(counts, dtype=np.uint32)
+    return g
+
+
 def make_copies(src_offsets, dst_offsets, lengths) -> np.ndarray:
     """Host array of smol_csum_copy_t (view it as uint8 and copy it to the device)."""
     n = len(src_offsets)
@@ -172,6 +186,36 @@ class ChecksumEngine:
                                               copies.data_ptr(), ctypes.byref(c),
                                               status.data_ptr() if status is not None else None,
                                               self._stream(stream)), "smol_csum_batch_copy_emit")
+        return status
+
+    def emit_frag(self, buf, batch: Batch, groups, caps=None, status=None, stream=None):
+        """IPv4 fragment groups (smol_csum_batch_emit_frag): ``groups`` is a device uint8 tensor of
+        smol_csum_frag_group_t (see make_groups).  Fills every fragment's header and each
+        datagram's L4 checksum; returns ``status`` (may be None)."""
+        self._check_buf(buf, batch)
+        assert groups.is_cuda and groups.numel() % 16 == 0
+        b = batch.c()
+        c = _caps(caps)
+        check(lib().smol_csum_batch_emit_frag(self._h, buf.data_ptr(), ctypes.byref(b), groups.data_ptr(),
+                                              groups.numel() // 16, ctypes.byref(c),
+                                              status.data_ptr() if status is not None else None,
+                                              self._stream(stream)), "smol_csum_batch_emit_frag")
+        return status
+
+    def verify_frag(self, buf, batch: Batch, groups, caps=None, status=None, stream=None):
+        """IPv4 fragment groups (smol_csum_batch_verify_frag): status bytes of every grouped record
+        (records outside the groups keep their value; a fresh status tensor starts zeroed)."""
+        import torch
+
+        self._check_buf(buf, batch)
+        assert groups.is_cuda and groups.numel() % 16 == 0
+        if status is None:
+            status = torch.zeros(batch.n, dtype=torch.uint8, device=buf.device)
+        b = batch.c()
+        c = _caps(caps)
+        check(lib().smol_csum_batch_verify_frag(self._h, buf.data_ptr(), ctypes.byref(b), groups.data_ptr(),
+                                                groups.numel() // 16, ctypes.byref(c), status.data_ptr(),
+                                                self._stream(stream)), "smol_csum_batch_verify_frag")
         return status
 
     def nhc_udp_emit(self, buf, batch: Batch, addrs, caps=None, status=None, stream=None):

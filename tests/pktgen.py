@@ -66,6 +66,32 @@ def icmp6(t: int, body_len: int, rng, csum: int = 0) -> bytes:
     return bytes([t, 0]) + be16(csum) + rand_bytes(rng, body_len)
 
 
+def fragment_like_iface(dgram: bytes, ip_mtu: int, ident: int, fill_header: bool):
+    """Cut an IPv4 datagram (20-byte header + the L4 bytes, as emit_ip left it in frag.buffer) the
+    way smoltcp's iface sends it: dispatch_ip's first fragment (src/iface/interface/mod.rs:1276-1331)
+    and dispatch_ipv4_frag's others (src/iface/interface/ipv4.rs:440-490).  Fragment data is
+    max_ipv4_fragment_size (src/phy/mod.rs:297-300: the payload MTU rounded down to 8 bytes); each
+    header is the datagram's with total length, ident, MF, DF = 0 and the offset rewritten, its
+    checksum filled when caps.ipv4.tx() (`fill_header`), else left 0 as Ipv4Repr::emit wrote it."""
+    from oracle import pyref
+
+    hdr, data = bytearray(dgram[:20]), dgram[20:]
+    step = (ip_mtu - 20) - (ip_mtu - 20) % 8
+    frags = []
+    for off in range(0, len(data), step):
+        part = data[off: off + step]
+        h = bytearray(hdr)
+        h[2:4] = (20 + len(part)).to_bytes(2, "big")
+        h[4:6] = ident.to_bytes(2, "big")
+        more = off + step < len(data)
+        h[6:8] = ((0x2000 if more else 0) | (off // 8)).to_bytes(2, "big")
+        h[10:12] = b"\0\0"
+        if fill_header:
+            pyref.ipv4_fill(h)
+        frags.append(bytes(h) + part)
+    return frags
+
+
 def eth(payload: bytes, ethertype: int = 0x0800) -> bytes:
     return bytes([0x02, 0, 0, 0, 0, 1, 0x02, 0, 0, 0, 0, 2]) + be16(ethertype) + payload
 

@@ -101,3 +101,121 @@ def test_fragment_refill_and_reassembly(eng, mtu):
         assert data == d[20:]
     _, rst = _device_emit(eng, [d for d in whole], gap_seed=3)
     assert all(s & E.ST_ACCEPT for s in rst)
+
+
+# ---------------------------------------------------------------------------------------------
+# Fragment groups through the drop-in route (smol_csum_batch_emit_frag / _verify_frag): the iface
+# fragments first with the L4 field and every header checksum written 0 by the offloaded caps;
+# the device fills each group; the bytes must equal the reference's "emit whole, then fragment".
+# ---------------------------------------------------------------------------------------------
+
+from tests import test_frag_cpu as F  # noqa: E402
+
+
+def _groups_dev(groups):
+    g = E.make_groups([f for f, _ in groups], [c for _, c in groups])
+    return torch.from_numpy(g.view(np.uint8).copy()).cuda(), g
+
+
+def _device_frag(eng, recs, groups, kind, caps=(0, 0, 0, 0, 0), seed=0):
+    buf, offs, lens = P.pack(recs, gap_rng=np.random.default_rng(seed))
+    batch = E.Batch.from_records(offs, lens, kind, "cuda:0")
+    gd, gh = _groups_dev(groups)
+    d = torch.from_numpy(buf.copy()).cuda()
+    st = torch.zeros(len(recs), dtype=torch.uint8, device="cuda:0")
+    eng.emit_frag(d, batch, gd, caps=caps, status=st)
+    got = d.cpu().numpy()
+    ref = buf.copy()
+    desc = P.oracle_desc(offs, lens, kind)
+    ref_st = oracle.batch_emit_frag(ref, desc, len(desc), gh, caps=caps)
+    diff = np.nonzero(got != ref)[0]
+    assert diff.size == 0, diff[:8]
+    assert np.array_equal(st.cpu().numpy(), ref_st)
+    vst = eng.verify_frag(d, batch, gd, caps=caps).cpu().numpy()
+    assert np.array_equal(vst, oracle.batch_verify_frag(ref, desc, len(desc), gh, caps=caps))
+    return got, offs, lens, vst
+
+
+@pytest.mark.parametrize("mtu,eth", [(576, False), (1280, True), (1500, False), (68, True)])
+def test_group_emit_drop_in_route(eng, mtu, eth):
+    rng = np.random.default_rng(mtu + 1)
+    small = mtu == 68
+    dg = F.datagrams(rng, 40, 60 if small else 600, 900 if small else 8000)
+    off, ref, groups = F.tx_pair(dg, mtu, eth, shuffle_rng=rng)
+    got, offs, lens, vst = _device_frag(eng, off, groups, E.KIND_ETH if eth else E.KIND_IP, seed=mtu)
+    for o, ln, want in zip(offs, lens, ref):
+        assert got[int(o):int(o) + int(ln)].tobytes() == want
+    assert (vst & E.ST_ACCEPT).all()
+
+
+def test_group_caps_and_one_record_groups(eng):
+    """Every caps row; groups of one unfragmented packet mixed with fragmented datagrams."""
+    rng = np.random.default_rng(11)
+    dg = F.datagrams(rng, 24, 300, 3000)
+    off, _, groups = F.tx_pair(dg, 1280, shuffle_rng=rng)
+    singles = [F.emit_whole(d, F.IGNORED) for d in F.datagrams(rng, 8, 20, 1200)]
+    recs = off + singles
+    groups = groups + [(len(off) + i, 1) for i in range(len(singles))]
+    for caps in ((0, 0, 0, 0, 0), (3, 0, 0, 0, 0), (0, 3, 3, 3, 0), (2, 1, 2, 1, 3), (1, 2, 1, 2, 0)):
+        _device_frag(eng, recs, groups, E.KIND_IP, caps=caps, seed=sum(caps))
+
+
+def test_group_verify_rejects_corrupted_and_broken(eng):
+    """RX: a corrupted reassembled datagram is rejected for every fragment, a corrupted header only
+    drops its datagram, and groups that break the contract are MALFORMED — all as the oracle."""
+    rng = np.random.default_rng(12)
+    dg = F.datagrams(rng, 30, 1500, 6000)
+    _, ref, groups = F.tx_pair(dg, 576, shuffle_rng=rng)
+    recs = [bytearray(r) for r in ref]
+    for gi, (f, c) in enumerate(groups):
+        if gi % 3 == 0:  # payload flip somewhere in the datagram
+            r = recs[f + int(rng.integers(c))]
+            r[20 + int(rng.integers(len(r) - 20))] ^= 1 << int(rng.integers(8))
+        elif gi % 3 == 1:  # header flip (TTL) in one fragment
+            recs[f + int(rng.integers(c))][8] ^= 0x04
+    recs = [bytes(r) for r in recs]
+    # contract breakers appended: a missing fragment, a duplicate, an ident mismatch
+    _, extra, eg = F.tx_pair(F.datagrams(rng, 3, 2500, 2600), 576)
+    base = len(recs)
+    (f0, c0), (f1, c1), (f2, c2) = eg
+    broken = [extra[f0:f0 + c0 - 1], extra[f1:f1 + c1] + [extra[f1]],
+              [extra[f2][:4] + b"\x55\x55" + extra[f2][6:]] + extra[f2 + 1:f2 + c2]]
+    for b in broken:
+        groups.append((base, len(b)))
+        recs += b
+        base += len(b)
+    buf, offs, lens = P.pack(recs, gap_rng=np.random.default_rng(5))
+    batch = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0")
+    gd, gh = _groups_dev(groups)
+    d = torch.from_numpy(buf.copy()).cuda()
+    for caps in ((0, 0, 0, 0, 0), (2, 0, 0, 0, 0), (0, 2, 2, 2, 0)):
+        vst = eng.verify_frag(d, batch, gd, caps=caps).cpu().numpy()
+        desc = P.oracle_desc(offs, lens, E.KIND_IP)
+        assert np.array_equal(vst, oracle.batch_verify_frag(buf, desc, len(desc), gh, caps=caps)), caps
+        if caps == (0, 0, 0, 0, 0):
+            for gi, (f, c) in enumerate(groups[:30]):
+                assert bool((vst[f:f + c] & E.ST_ACCEPT).all()) == (gi % 3 == 2), gi
+            assert (vst[len(ref):] & E.ST_MALFORMED).all()
+
+
+def test_group_fixed_stride(eng):
+    """Fragment records at a fixed stride (a device RX ring), groups over them."""
+    rng = np.random.default_rng(13)
+    off, ref, groups = F.tx_pair(F.datagrams(rng, 20, 1000, 5000), 1500, shuffle_rng=rng)
+    stride = 1501
+    host = np.zeros(len(off) * stride + 64, np.uint8)
+    for i, r in enumerate(off):
+        host[i * stride:i * stride + len(r)] = np.frombuffer(r, np.uint8)
+    # records shorter than the stride: the IP total length decides, the rest is slack
+    d = torch.from_numpy(host.copy()).cuda()
+    batch = E.Batch.fixed(len(off), stride, stride, E.KIND_IP)
+    gd, gh = _groups_dev(groups)
+    eng.emit_frag(d, batch, gd)
+    got = d.cpu().numpy()
+    want = host.copy()
+    oracle.batch_emit_frag(want, None, len(off), gh, stride=stride, length=stride, kind=1)
+    assert np.array_equal(got, want)
+    for i, r in enumerate(ref):
+        assert got[i * stride:i * stride + len(r)].tobytes() == r
+    vst = eng.verify_frag(d, batch, gd).cpu().numpy()
+    assert (vst & E.ST_ACCEPT).all()
