@@ -206,6 +206,27 @@ public:
         check(smol_csum_batch_verify(ctx_, d_buf, &bc, &cc, d_status, stream), "smol_csum_batch_verify");
     }
 
+    // IPv4 fragment groups: d_groups[k] = one datagram's fragments (consecutive records).  Fills every
+    // fragment header and each datagram's L4 checksum over its reassembled payload (the iface's
+    // "emit whole, then fragment", src/iface/interface/mod.rs:1276-1331).
+    void emit_frag(uint8_t* d_buf, const Batch& b, const smol_csum_frag_group_t* d_groups, uint64_t n_groups,
+                   const smoltcp::phy::ChecksumCapabilities& caps = {}, uint8_t* d_status = nullptr,
+                   void* stream = nullptr) {
+        auto bc = b.c();
+        auto cc = caps.c();
+        check(smol_csum_batch_emit_frag(ctx_, d_buf, &bc, d_groups, n_groups, &cc, d_status, stream),
+              "smol_csum_batch_emit_frag");
+    }
+    // Fragment headers + the reassembled datagram's L4 gate (src/iface/interface/ipv4.rs:103-146).
+    void verify_frag(const uint8_t* d_buf, const Batch& b, const smol_csum_frag_group_t* d_groups,
+                     uint64_t n_groups, uint8_t* d_status, const smoltcp::phy::ChecksumCapabilities& caps = {},
+                     void* stream = nullptr) {
+        auto bc = b.c();
+        auto cc = caps.c();
+        check(smol_csum_batch_verify_frag(ctx_, d_buf, &bc, d_groups, n_groups, &cc, d_status, stream),
+              "smol_csum_batch_verify_frag");
+    }
+
     // 6LoWPAN NHC UDP (sixlowpan::nhc::UdpNhcRepr::emit / ::parse): every record is a LOWPAN_NHC
     // UDP packet; d_addrs[i] holds record i's IPv6 addresses (IPHC-decompressed).
     void nhc_udp_emit(uint8_t* d_buf, const Batch& b, const smol_ipv6_addr_pair_t* d_addrs,
