@@ -82,13 +82,21 @@ constexpr uint32_t kNaturalGrid = 0x7fffffffu;
 // verify is slower, 1.08 ms vs 0.83 ms).  walk_variant is the walk kernel's own choice, for the
 // entry points the tile kernel does not serve (NHC, data, copy-emit): cached loads on the 16-byte
 // grid for emit over descriptors (C3 0.9705 ms vs 0.9722 ms), the line grid otherwise.
-int walk_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 1 : 5; }
-int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : 5; }
+// Verify over descriptor batches (C3) runs the line grid without the register prefetch (variant
+// 13) at 16 x 4: with the record geometry in LDS that kernel holds 63 VGPRs (8 waves/SIMD), and the
+// waves hide the latency the prefetch hid before: C3 verify 0.7998 ms (variant 5, 16 x 3) ->
+// 0.7425 ms (tools/gpu_ab.sh, MI355X).  Fixed-stride verify keeps the prefetch (C2 8 x 7: 0.2378
+// vs 0.2519 ms without).
+int walk_variant(int mode, bool has_desc) {
+    if (!has_desc) return 5;
+    return mode == MODE_EMIT ? 1 : mode == MODE_VERIFY ? 13 : 5;
+}
+int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
-bool line_grid(int variant) { return variant == 5 || variant == 6 || variant == 9 || variant == 10; }
+bool line_grid(int variant) { return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13; }
 
-int auto_shape(uint32_t len, bool has_desc, bool line = false) {
-    if (has_desc) return CFG_G16U3;
+int auto_shape(uint32_t len, bool has_desc, bool line = false, int variant = -1) {
+    if (has_desc) return variant == 13 ? CFG_G16U4 : CFG_G16U3;
     const uint64_t need = (uint64_t)len + (line ? 127 : 15);  // bytes of aligned chunks a record can touch
     // eight records per wavefront in two steps, with as few idle lanes as possible (C4's 1320-B
     // records on the line grid: 8 x 6 0.2083 ms, 8 x 7 0.2188 ms; C2's 1500 B: 8 x 7 0.2327 ms)
@@ -149,10 +157,13 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
     if (tile_var && (mode == MODE_DATA || mode == MODE_COPY || d_addrs)) variant = walk_variant(mode, has_desc);
     const bool use_tile = variant == 3 || variant == 4 || variant == 7;
-    int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, has_desc, line_grid(variant));
+    int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, has_desc, line_grid(variant), variant);
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
-        hipError_t e = launch_csum(MODE_COPY, shape, ctx->variant == 1 ? 1 : 8, p, ctx->max_blocks, s);
+        // default: variant 11 (no prefetch, the second source chunk from the neighbour lane):
+        // C2copy 0.910 -> 0.838 ms against variant 8 (tools/exp_copy.py, MI355X)
+        const int cv = ctx->variant;
+        hipError_t e = launch_csum(MODE_COPY, shape, (cv == 1 || cv == 8 || cv == 12) ? cv : 11, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
     }
@@ -366,7 +377,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 10) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 13) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }
@@ -395,7 +406,8 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
 }
 
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
-    return auto_shape(len, has_desc != 0, line_grid(auto_variant(MODE_VERIFY, has_desc != 0)));
+    const int v = auto_variant(MODE_VERIFY, has_desc != 0);
+    return auto_shape(len, has_desc != 0, line_grid(v), v);
 }
 
 const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int has_desc) {

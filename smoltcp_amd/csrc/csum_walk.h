@@ -51,12 +51,17 @@ namespace smolcsum {
 // 9 / 10 = variant 5 with the first two / the first chunk of every lane's step loaded cached
 // (fixed-stride emit only: the 128-B line(s) holding the two fields stay resident in L2 when the
 // field stores arrive; measured in DESIGN.md §5).
+// 13 = variant 5 without the register prefetch.
+// 11 / 12 = MODE_COPY on the 16-byte grid, plain loads, without / with the register prefetch, each
+// source chunk loaded once: a lane takes the second source chunk of its funnel shift from the next
+// lane of its group (DPP / ds_bpermute) instead of loading it again.
 template <int VAR>
 struct VarT {
-    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10;
-    static constexpr bool PF = VAR != 2 && VAR != 8;
-    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10;
+    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13;
+    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13;
+    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13;
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
+    static constexpr bool SHUF = VAR == 11 || VAR == 12;
 };
 
 template <bool LINE>
@@ -141,6 +146,7 @@ struct Regs {
 template <int U>
 struct Regs<U, true> {
     u32x4 v[U], s0[U], s1[U];
+    u32x4 sx;  // SHUF: lane 0's source chunk for the chunk after the step (the group's last lane needs it)
 };
 
 // Issue the U loads of one step.  Unconditional: chunks past the record (or a step that does
@@ -149,12 +155,33 @@ struct Regs<U, true> {
 // payload bytes (so no load ever leaves the source range's aligned chunks).
 // Chunks at addresses >= lim are not loaded (they come from the next record's LDS window, see
 // shared_from).
-template <int G, int U, bool NT, bool COPY, bool LINE, int CACHED_U = 0>
+// SHUF (MODE_COPY): each lane loads the aligned source chunk under its chunk's first byte whenever it
+// lies in the source range's aligned chunks, payload or not (its left neighbour may need it), and
+// lane 0 also loads the one under the chunk after the step (sx).
+template <int G, int U, bool NT, bool COPY, bool LINE, int CACHED_U = 0, bool SHUF = false>
 __device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, uint32_t nch,
                                           uint32_t step, int lane, bool valid, uint64_t dummy,
                                           uint64_t lim = ~0ull) {
     static_assert(!(COPY && LINE), "MODE_COPY uses the 16-byte grid");
     const uint64_t base = rr.a0 & ~(Grid<LINE>::ALIGN - 1);
+    if constexpr (COPY && SHUF) {
+        const bool pay = valid && rr.p1 > rr.p0;
+        const uint64_t first = (rr.sb + rr.p0) & ~15ull, last = (rr.sb + rr.p1 - 1) & ~15ull;
+        const uint64_t sk = rr.sb - (rr.a0 & 15u);  // source address of chunk 0's byte 0
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = step * (G * U) + u * G + lane;
+            const bool in = valid && k < nch;
+            const int64_t pos = (int64_t)(16u * k) - (int64_t)(rr.a0 & 15u);
+            const bool full = pos >= (int64_t)rr.p0 && pos + 16 <= (int64_t)rr.p1;
+            R.v[u] = ld16<NT>((gcv4)(in && !full ? base + 16ull * k : dummy));
+            const uint64_t sA = (sk + 16ull * k) & ~15ull;
+            R.s0[u] = ld16<NT>((gcv4)(pay && sA >= first && sA <= last ? sA : dummy));
+        }
+        const uint64_t sX = (sk + 16ull * ((step + 1) * (G * U))) & ~15ull;
+        R.sx = ld16<NT>((gcv4)(pay && lane == 0 && (sk & 15u) && sX >= first && sX <= last ? sX : dummy));
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t k = step * (G * U) + u * G + lane;
@@ -229,6 +256,21 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v) {
     return v;
 }
 
+// The value x of lane (lane + 1) mod G of the caller's group (every lane of the group active).
+template <int G>
+__device__ __forceinline__ uint32_t group_next(uint32_t x, int lane) {
+    if constexpr (G == 8) {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, false);  // row_shl:1
+        const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x117, 0xF, 0xF, false);  // row_shr:7
+        return lane == G - 1 ? b : a;
+    } else if constexpr (G == 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x12F, 0xF, 0xF, false);  // row_ror:15
+    } else {
+        const int src = (int)(threadIdx.x & 63u) - lane + ((lane + 1) & (G - 1));
+        return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)x);
+    }
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -260,7 +302,8 @@ struct Walk {
     RecRef cur, nxt; // current record, the group's next record (descriptor prefetched)
     uint32_t nch;    // aligned chunks of cur
     uint32_t step;   // step within cur
-    Geom g;          // cur's geometry (protocol modes)
+    Geom* g;         // cur's geometry (protocol modes) in LDS: 13 VGPRs less across the walk
+    Geom gr;         // ... or in registers (MODE_EMIT: measured faster there, see csum_kernel)
     int s1;          // end of the summed span, relative to the record start
     uint32_t acc, acc2;
     uint32_t fip, fl4, fin;  // MODE_COPY: record offsets of the fields emit writes (NO_FIELD if none)
@@ -454,11 +497,13 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
-template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0>
+template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
+          bool SHUF = false>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib) {
     constexpr bool COPY = MODE == MODE_COPY;
+    constexpr bool GREG = MODE == MODE_EMIT;  // where the record geometry lives (Walk::g / Walk::gr)
     constexpr int WIN = Grid<LINE>::WIN;
     constexpr int WIN_CH = Grid<LINE>::WIN_CH;
     static_assert(G * U >= WIN_CH, "step 0 must cover the LDS window");
@@ -473,7 +518,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     // SKIPD: no prefetch when the group has nothing left (one record per group in a natural grid:
     // every record's last step would otherwise issue U loads of the dummy line)
     if (PF && (!SKIPD || have2))
-        load_step<G, U, NT, COPY, LINE, CU>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
+        load_step<G, U, NT, COPY, LINE, CU, SHUF>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
                                             shared_from<G, MODE, IMPLICIT, LINE>(p, r2, rec2.a0, gib, ngroups));
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
@@ -497,6 +542,18 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 #pragma unroll
     for (int u = 0; u < U; ++u) cm[u] = cv.v[u];
     if constexpr (COPY) {
+        if constexpr (SHUF) {
+            // the second source chunk of lane i's funnel is lane i+1's first (the group's last lane:
+            // lane 0's next one), taken with all lanes of the group active
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32x4 x = lane == 0 ? (u + 1 < U ? cv.s0[u + 1 < U ? u + 1 : u] : cv.sx) : cv.s0[u];
+                cv.s1[u].x = group_next<G>(x.x, lane);
+                cv.s1[u].y = group_next<G>(x.y, lane);
+                cv.s1[u].z = group_next<G>(x.z, lane);
+                cv.s1[u].w = group_next<G>(x.w, lane);
+            }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t k = w.step * (G * U) + u * G + lane;
@@ -529,17 +586,23 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             }
             wave_lds_sync();
             if (COPY && (w.cur.kind & KIND_BAD_COPY)) {
-                w.g = Geom{};
-                w.g.st = SMOL_ST_MALFORMED;  // copy range does not fit: record left untouched
+                Geom g0 = Geom{};
+                g0.st = SMOL_ST_MALFORMED;  // copy range does not fit: record left untouched
+                if (lane == 0) *w.g = g0;
+            } else if constexpr (GREG) {
+                w.gr = parse_geometry<NHC>(rd, w.cur.len, w.cur.kind, true);
             } else {
-                w.g = parse_geometry<NHC>(rd, w.cur.len, w.cur.kind, MODE == MODE_EMIT || MODE == MODE_COPY);
+                const Geom g0 = parse_geometry<NHC>(rd, w.cur.len, w.cur.kind, MODE == MODE_EMIT || MODE == MODE_COPY);
+                if (lane == 0) *w.g = g0;
             }
+            if (!GREG) wave_lds_sync();
+            const Geom& g = GREG ? w.gr : *w.g;
             // the lanes sum [0, span_end): the header part is subtracted at the end
-            w.s1 = (w.g.proto != P_NONE && !(w.g.st & SMOL_ST_MALFORMED)) ? (int)w.g.span_end : 0;
+            w.s1 = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? (int)g.span_end : 0;
             if (COPY) {
-                w.fip = w.g.fam == 4 ? w.g.ip_off + 10 : NO_FIELD;
-                w.fl4 = (w.g.proto != P_NONE && !(w.g.st & SMOL_ST_MALFORMED)) ? w.g.l4_off + w.g.fo : NO_FIELD;
-                w.fin = w.g.in_off ? w.g.in_off + 10 : NO_FIELD;
+                w.fip = g.fam == 4 ? g.ip_off + 10 : NO_FIELD;
+                w.fl4 = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? g.l4_off + g.fo : NO_FIELD;
+                w.fin = g.in_off ? g.in_off + 10 : NO_FIELD;
             }
         }
     }
@@ -618,7 +681,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const uint32_t tot = group_sum<G>(s_rel);
             if (lane == 0) ((gu16)p.out16)[r] = (uint16_t)bswap16(fold32(tot));
         } else {
-            finish_gates<G, MODE, NHC>(p, w.g, w.acc, rd, winb, head, w.cur.a0, r, lane);
+            finish_gates<G, MODE, NHC>(p, GREG ? w.gr : *w.g, w.acc, rd, winb, head, w.cur.a0, r, lane);
         }
     }
 
@@ -640,6 +703,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool PF = VarT<VAR>::PF;
     constexpr bool LINE = VarT<VAR>::LINE;
     constexpr int CU = VarT<VAR>::CACHED_U;
+    constexpr bool SHUF = VarT<VAR>::SHUF;
     // Fixed-stride batches: no prefetch once the group has nothing left (one record per group in
     // a natural grid), measured 1-1.5 % faster (C2 verify 0.2444 -> 0.2422 ms, C4 0.2219 -> 0.2189
     // ms).  Descriptor batches keep the unconditional prefetch: there the conditional load made
@@ -649,6 +713,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr int GPB = 256 / G;
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     __shared__ u32x4 win[GPB][Grid<LINE>::WIN_CH];
+    __shared__ Geom geo[GPB];
 
     const int lane = (int)(threadIdx.x % G);
     const int gib = (int)(threadIdx.x / G);
@@ -660,7 +725,11 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     w.nxt = rec_at<IMPLICIT, COPY, NHC>(p, w.r + ngroups < p.n ? w.r + ngroups : p.n - 1);
     w.nch = n_chunks<LINE>(w.cur);
     w.step = 0;
-    w.g = Geom{};
+    // The record geometry: in LDS, except for emit.  Measured (tools/gpu_ab.sh, MI355X): in LDS,
+    // C4 verify 0.2167 -> 0.2044 ms (8 x 6: 113 -> 95 VGPRs, 4 -> 5 waves/SIMD) but C4 emit
+    // 0.2656 -> 0.2738 ms; C2 (8 x 7) unchanged either way.
+    w.g = &geo[gib];
+    w.gr = Geom{};
     w.s1 = 0;
     w.acc = w.acc2 = 0;
     w.fip = w.fl4 = w.fin = NO_FIELD;
@@ -668,18 +737,18 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     Regs<U, COPY> va;
     if (PF) {
         Regs<U, COPY> vb;
-        load_step<G, U, NT, COPY, LINE, CU>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
-                                            shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
+        load_step<G, U, NT, COPY, LINE, CU, SHUF>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
+                                                  shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU>(p, w, va, vb, lane, ngroups, &win[gib][0], gib)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU>(p, w, vb, va, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF>(p, w, va, vb, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF>(p, w, vb, va, lane, ngroups, &win[gib][0], gib)) break;
         }
     } else {
         while (true) {
-            load_step<G, U, NT, COPY, LINE>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
-                                            shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC>(p, w, va, va, lane, ngroups, &win[gib][0], gib)) break;
+            load_step<G, U, NT, COPY, LINE, 0, SHUF>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
+                                                     shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF>(p, w, va, va, lane, ngroups, &win[gib][0], gib)) break;
         }
     }
 }
@@ -719,6 +788,7 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 2: return launch_shape<MODE, IMPLICIT, 2>(shape, p, max_blocks, s);
         case 5: return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
+        case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
         case 9:
         case 10:
             if constexpr (MODE == MODE_EMIT && IMPLICIT) {
@@ -767,8 +837,12 @@ hipError_t launch_copy_var(int shape, const KParams& p, uint32_t max_blocks, hip
 
 template <bool IMPLICIT>
 hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    return var == 1 ? launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s)
-                    : launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);
+    switch (var) {
+        case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
+        case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);
+        case 12: return launch_copy_var<IMPLICIT, 12>(shape, p, max_blocks, s);
+        default: return launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);
+    }
 }
 
 }  // namespace smolcsum

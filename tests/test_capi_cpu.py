@@ -123,7 +123,7 @@ def test_auto_shape():
     assert auto_shape(1500) == 7    # 8 x 7: eight 1500-byte records per wavefront, two steps each
     assert auto_shape(1900) == 4    # 32 x 4 (line grid: up to 2048 - 127 bytes)
     assert auto_shape(9000) == 6    # 64 x 4
-    assert auto_shape(1500, True) == 1  # descriptors: 16 x 3
+    assert auto_shape(1500, True) == 8  # descriptors: 16 x 4 (verify: line grid, no prefetch)
 
 
 def test_phy_policy_mirror():

@@ -175,24 +175,30 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
     rng = np.random.default_rng(stride + length)
     for n, base in ((1, 0), (2, 5), (33, 64), (1029, 3), (2048, 0)):
         recs, spec = _fixed_case(rng, n, length)
-        for variant, blocks in ((-1, 0), (-1, 7), (1, 0)):  # default (variant 8) and the prefetch variant
+        # the default, a capped grid, the prefetch variant and the lane-shuffle variants (11 / 12)
+        for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (12, 0), (12, 7), (8, 0)):
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,
                  base=base, seed=n + variant)
 
 
+COPY_VARIANTS = [-1, 1, 8, 11, 12]
+
+
+@pytest.mark.parametrize("variant", COPY_VARIANTS)
 @pytest.mark.parametrize("shape", [-1, 0, 1, 3, 5])
-def test_copy_emit_mixed_packed(eng, shape):
+def test_copy_emit_mixed_packed(eng, shape, variant):
     rng = np.random.default_rng(10 + shape)
     recs, spec = [], []
     for i in range(1200):
         r, hdr = _packet(rng, i)
         recs.append(r)
         spec.append((hdr, len(r) - hdr))
-    st, got, offs, lens = _run(eng, recs, spec, shape=shape, gap_seed=3, seed=4)
+    st, got, offs, lens = _run(eng, recs, spec, shape=shape, gap_seed=3, seed=4, variant=variant)
     assert (st & E.ST_MALFORMED).sum() == 0
 
 
-def test_copy_emit_all_alignments(eng):
+@pytest.mark.parametrize("variant", COPY_VARIANTS)
+def test_copy_emit_all_alignments(eng, variant):
     """dst offsets and source offsets cover every residue mod 16."""
     rng = np.random.default_rng(7)
     recs, spec = [], []
@@ -202,10 +208,12 @@ def test_copy_emit_all_alignments(eng):
         recs.append(r)
         d0 = 40 - (i % 16)  # copy part of the header too: ranges start anywhere in the TCP header
         spec.append((d0, len(r) - d0 - (i % 5)))
-    _run(eng, recs, spec, gap_seed=9, seed=11)
+    for shape in (-1, 0, 5):
+        _run(eng, recs, spec, gap_seed=9, seed=11, variant=variant, shape=shape)
 
 
-def test_copy_over_fields_and_edge_ranges(eng):
+@pytest.mark.parametrize("variant", COPY_VARIANTS)
+def test_copy_over_fields_and_edge_ranges(eng, variant):
     rng = np.random.default_rng(21)
     recs, spec = [], []
     for i in range(400):
@@ -228,7 +236,7 @@ def test_copy_over_fields_and_edge_ranges(eng):
             spec.append((1, len(r) - 1))
         else:
             spec.append((hdr, len(r) - hdr))
-    st, got, _, _ = _run(eng, recs, spec, gap_seed=5, seed=6)
+    st, got, _, _ = _run(eng, recs, spec, gap_seed=5, seed=6, variant=variant)
     assert ((st & E.ST_MALFORMED) != 0).sum() >= 50
 
 
@@ -246,7 +254,8 @@ def test_copy_emit_caps_and_rejected_records(eng):
         recs.append(r)
         spec.append((hdr, len(r) - hdr))
     for caps in [(3, 3, 3, 3, 3), (1, 2, 1, 2, 1), (0, 0, 0, 0, 0)]:
-        _run(eng, recs, spec, caps=caps, gap_seed=8, seed=12)
+        for variant in (-1, 11):
+            _run(eng, recs, spec, caps=caps, gap_seed=8, seed=12, variant=variant)
 
 
 def test_copy_emit_errors(eng):

@@ -207,16 +207,22 @@ def test_packed_mixed_lengths_descriptors(eng):
     eng.corrupt(buf, batch, every=7, seed=3)
     host = buf.cpu().numpy().copy()
     desc = E.make_descriptors(offs, lens, E.KIND_IP)
-    for shape in SHAPES:
-        eng.set_shape(shape)
-        st = eng.verify(buf, batch).cpu().numpy()
-        assert np.array_equal(st, oracle.batch_verify(host, desc, n)), shape
-        d2 = buf.clone()
-        eng.emit(d2, batch)
-        ref = host.copy()
-        oracle.batch_emit(ref, desc, n)
-        assert np.array_equal(d2.cpu().numpy(), ref), shape
-    eng.set_shape(-1)
+    ref_v = oracle.batch_verify(host, desc, n)
+    ref = host.copy()
+    oracle.batch_emit(ref, desc, n)
+    for variant in (-1, 5, 13, 1):
+        for shape in SHAPES:
+            eng.set_shape(shape)
+            eng.set_variant(variant)
+            try:
+                st = eng.verify(buf, batch).cpu().numpy()
+                d2 = buf.clone()
+                eng.emit(d2, batch)
+            finally:
+                eng.set_shape(-1)
+                eng.set_variant(-1)
+            assert np.array_equal(st, ref_v), (variant, shape)
+            assert np.array_equal(d2.cpu().numpy(), ref), (variant, shape)
 
 
 def test_persistent_grid_small(eng):
@@ -536,7 +542,7 @@ def test_emit_large_batch(eng):
         _emit_case(eng, host, off, n, stride, L, E.KIND_IP, CAPS_DEFAULT, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 13])
 def test_variants_fixed_stride(eng, variant):
     """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
     the oracle on fixed-stride batches: strides equal to the record length (neighbours share

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Time the fused copy + emit (C2copy workload) for every launch shape: one JSON line per shape."""
+"""Time the fused copy + emit (C2copy workload) per launch shape and kernel variant: one JSON line each.
+
+Usage: exp_copy.py [shapes, e.g. 0,1,3,5] [variants, e.g. 8,11,12]"""
 import json
 import os
 import sys
@@ -20,8 +22,11 @@ def main():
     eng.synth(tx, b, E.SYNTH_UDP4, 0x5EED0006)
     src = torch.randint(0, 256, (n * 1472 + 16,), dtype=torch.uint8, device=dev)
     cp = torch.from_numpy(E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472).view(np.uint8).copy()).to(dev)
-    for shape in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,3,5").split(",")]:
+    variants = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "-1").split(",")]
+    shapes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,3,5").split(",")]
+    for rnd, shape, var in [(r, s, v) for r in range(3) for s in shapes for v in variants]:
         eng.set_shape(shape)
+        eng.set_variant(var)
         for _ in range(3):
             eng.copy_emit(tx, b, src, cp)
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -32,7 +37,7 @@ def main():
         torch.cuda.synchronize()
         ms = a.elapsed_time(z) / 20
         moved = n * (28 + 1472 + 1472 + 4)
-        print(json.dumps({"shape": shape, "ms": round(ms, 4), "GBs_rw": round(moved / ms / 1e6, 1)}), flush=True)
+        print(json.dumps({"round": rnd, "shape": shape, "variant": var, "ms": round(ms, 4), "GBs_rw": round(moved / ms / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
