@@ -52,16 +52,21 @@ namespace smolcsum {
 // (fixed-stride emit only: the 128-B line(s) holding the two fields stay resident in L2 when the
 // field stores arrive; measured in DESIGN.md §5).
 // 13 = variant 5 without the register prefetch.
-// 11 / 12 = MODE_COPY on the 16-byte grid, plain loads, without / with the register prefetch, each
-// source chunk loaded once: a lane takes the second source chunk of its funnel shift from the next
-// lane of its group (DPP / ds_bpermute) instead of loading it again.
+// MODE_COPY (16-byte grid, plain loads, no register prefetch): 8 = two aligned source chunks per
+// destination chunk; 11 = one, the second taken from the next lane of the group (DPP /
+// ds_bpermute); 16 (the default) = variant 11 with dword-aligned source loads — a lane loads the 16
+// source bytes from its chunk's first source byte rounded down to 4 (an unaligned 16-byte load), so
+// the funnel is four v_alignbyte and only ONE dword comes from the next lane — and every byte of
+// the record written (WHOLE, see walk_step).  Measured variants that lost are in DESIGN.md §6.
 template <int VAR>
 struct VarT {
     static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13;
-    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13;
+    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16;
     static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13;
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
-    static constexpr bool SHUF = VAR == 11 || VAR == 12;
+    static constexpr bool SHUF = VAR == 11 || VAR == 16;
+    static constexpr bool WHOLE = VAR == 16;
+    static constexpr bool SHUF2 = VAR == 16;
 };
 
 template <bool LINE>
@@ -147,6 +152,7 @@ template <int U>
 struct Regs<U, true> {
     u32x4 v[U], s0[U], s1[U];
     u32x4 sx;  // SHUF: lane 0's source chunk for the chunk after the step (the group's last lane needs it)
+    uint32_t sx1;  // SHUF2: lane 0's first source dword of the chunk after the step
 };
 
 // Issue the U loads of one step.  Unconditional: chunks past the record (or a step that does
@@ -158,21 +164,44 @@ struct Regs<U, true> {
 // SHUF (MODE_COPY): each lane loads the aligned source chunk under its chunk's first byte whenever it
 // lies in the source range's aligned chunks, payload or not (its left neighbour may need it), and
 // lane 0 also loads the one under the chunk after the step (sx).
-template <int G, int U, bool NT, bool COPY, bool LINE, int CACHED_U = 0, bool SHUF = false>
+// SHUF2 (MODE_COPY): the source load of chunk k starts at A = (its first source byte) & ~3 when
+// [A, A + 16) lies inside the source range's aligned chunks [first, last + 16); otherwise (the
+// payload's first / last chunk) at first / last, and the merge shifts it there.  Lane 0 also loads
+// the dword at A of the chunk after the step (sx1), for the group's last lane.
+template <int G, int U, bool NT, bool COPY, bool LINE, int CACHED_U = 0, bool SHUF = false, bool SHUF2 = false>
 __device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, uint32_t nch,
                                           uint32_t step, int lane, bool valid, uint64_t dummy,
                                           uint64_t lim = ~0ull) {
     static_assert(!(COPY && LINE), "MODE_COPY uses the 16-byte grid");
     const uint64_t base = rr.a0 & ~(Grid<LINE>::ALIGN - 1);
-    if constexpr (COPY && SHUF) {
+    if constexpr (COPY && SHUF2) {
         const bool pay = valid && rr.p1 > rr.p0;
         const uint64_t first = (rr.sb + rr.p0) & ~15ull, last = (rr.sb + rr.p1 - 1) & ~15ull;
-        const uint64_t sk = rr.sb - (rr.a0 & 15u);  // source address of chunk 0's byte 0
+        const uint64_t sk = rr.sb - (rr.a0 - base);  // source address of chunk 0's byte 0
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t k = step * (G * U) + u * G + lane;
             const bool in = valid && k < nch;
-            const int64_t pos = (int64_t)(16u * k) - (int64_t)(rr.a0 & 15u);
+            const int64_t pos = (int64_t)(16u * k) - (int64_t)(rr.a0 - base);
+            const bool full = pos >= (int64_t)rr.p0 && pos + 16 <= (int64_t)rr.p1;
+            R.v[u] = ld16<NT>((gcv4)(in && !full ? base + 16ull * k : dummy));
+            const uint64_t sa = sk + 16ull * k, A = sa & ~3ull;
+            const uint64_t la = A < first ? first : A > last ? last : A;
+            R.s0[u] = ld16<NT>((gcv4)(pay && sa + 16 > first && A <= last + 12 ? la : dummy));
+        }
+        const uint64_t AX = (sk + 16ull * ((step + 1) * (G * U))) & ~3ull;
+        R.sx1 = *(const GMEM uint32_t*)(pay && lane == 0 && AX >= first && AX <= last + 12 ? AX : dummy);
+        return;
+    }
+    if constexpr (COPY && SHUF) {
+        const bool pay = valid && rr.p1 > rr.p0;
+        const uint64_t first = (rr.sb + rr.p0) & ~15ull, last = (rr.sb + rr.p1 - 1) & ~15ull;
+        const uint64_t sk = rr.sb - (rr.a0 - base);  // source address of chunk 0's byte 0
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = step * (G * U) + u * G + lane;
+            const bool in = valid && k < nch;
+            const int64_t pos = (int64_t)(16u * k) - (int64_t)(rr.a0 - base);
             const bool full = pos >= (int64_t)rr.p0 && pos + 16 <= (int64_t)rr.p1;
             R.v[u] = ld16<NT>((gcv4)(in && !full ? base + 16ull * k : dummy));
             const uint64_t sA = (sk + 16ull * k) & ~15ull;
@@ -307,6 +336,7 @@ struct Walk {
     int s1;          // end of the summed span, relative to the record start
     uint32_t acc, acc2;
     uint32_t fip, fl4, fin;  // MODE_COPY: record offsets of the fields emit writes (NO_FIELD if none)
+    bool far;                // MODE_COPY, WHOLE: a field lies (partly) past the LDS window
 };
 
 constexpr uint32_t NO_FIELD = 0x3fffffffu;
@@ -316,10 +346,12 @@ constexpr uint32_t MF_NONE = 0x3fffu;  // no field (finish_gates)
 // lane holds its part `acc` of the aligned-word sum over [0, span_end): the header bytes the lanes
 // summed are taken out again, the IPv4 header sum and the pseudo-header address words are read from
 // the LDS window (`winb`, record byte o at head + o), and lane 0 finishes and writes the record.
-template <int G, int MODE, bool NHC, class RD>
+// WINB > 0 (MODE_COPY, WHOLE): field bytes inside the first WINB bytes of the chunk grid go into the
+// LDS window (`winw`), whose chunks the caller stores afterwards, instead of to global memory.
+template <int G, int MODE, bool NHC, class RD, int WINB = 0>
 __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, uint32_t acc, const RD& rd,
                                              const uint8_t* winb, uint32_t head, uint64_t a0, uint64_t r,
-                                             int lane) {
+                                             int lane, uint8_t* winw = nullptr) {
     constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
     const bool odd = (a0 & 1u) != 0;
     // Header bytes [0, l4_off) that the lanes summed (taken out of the L4 sum), the IPv4
@@ -455,7 +487,19 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
                 l4_ok = caps_rx(gate_caps) ? l4_valid : 1u;
             }
         }
-        if (EMITS) {
+        if (EMITS && WINB > 0) {
+            auto put = [&](uint32_t f, uint32_t v) {
+                for (uint32_t i = 0; i < 2; ++i) {
+                    const uint8_t b = (uint8_t)(i ? v : v >> 8);
+                    if (head + f + i < (uint32_t)WINB) winw[head + f + i] = b;
+                    else wrec[f + i] = b;
+                }
+            };
+            if (fip != MF_NONE) put(fip, vip);
+            if (fin != MF_NONE) put(fin, vin);
+            if (fl4 != MF_NONE) put(fl4, vl4);
+            if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
+        } else if (EMITS) {
             if (fip != MF_NONE) store_be16(wrec + fip, vip);
             if (fin != MF_NONE) store_be16(wrec + fin, vin);
             if (fl4 != MF_NONE) store_be16(wrec + fl4, vl4);
@@ -498,7 +542,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
-          bool SHUF = false>
+          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib) {
@@ -518,7 +562,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     // SKIPD: no prefetch when the group has nothing left (one record per group in a natural grid:
     // every record's last step would otherwise issue U loads of the dummy line)
     if (PF && (!SKIPD || have2))
-        load_step<G, U, NT, COPY, LINE, CU, SHUF>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
+        load_step<G, U, NT, COPY, LINE, CU, SHUF, SHUF2>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
                                             shared_from<G, MODE, IMPLICIT, LINE>(p, r2, rec2.a0, gib, ngroups));
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
@@ -541,7 +585,56 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     u32x4 cm[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) cm[u] = cv.v[u];
-    if constexpr (COPY) {
+    if constexpr (COPY && SHUF2) {
+        const uint64_t first = (w.cur.sb + w.cur.p0) & ~15ull, last = (w.cur.sb + w.cur.p1 - 1) & ~15ull;
+        const uint64_t sk = w.cur.sb - head;  // source address of chunk 0's byte 0
+        const uint32_t b = (uint32_t)(sk & 3u);
+        // the dword at A of each lane's chunk (the next lane's funnel needs it): s0.x, or for a
+        // chunk loaded at `last`, the dword (A - last) / 4 of it
+        uint32_t xo[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = w.step * (G * U) + u * G + lane;
+            const uint64_t A = (sk + 16ull * k) & ~3ull;
+            const u32x4 c = cv.s0[u];
+            xo[u] = c.x;
+            if (A > last) {
+                const uint32_t q = (uint32_t)(A - last) >> 2;
+                xo[u] = q == 1 ? c.y : q == 2 ? c.z : c.w;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t nxd = group_next<G>(lane == 0 ? (u + 1 < U ? xo[u + 1 < U ? u + 1 : u] : cv.sx1) : xo[u], lane);
+            const uint32_t k = w.step * (G * U) + u * G + lane;
+            const int pos = (int)(16u * k) - (int)head;
+            const int lo = (int)w.cur.p0 - pos, hi = (int)w.cur.p1 - pos;
+            if (k < w.nch && w.cur.p1 > w.cur.p0 && hi > 0 && lo < 16) {
+                const uint64_t sa = sk + 16ull * k, A = sa & ~3ull;
+                const u32x4 c = cv.s0[u];
+                u32x4 src;
+                if (A >= first && A <= last) {
+                    src.x = __builtin_amdgcn_alignbyte(c.y, c.x, b);
+                    src.y = __builtin_amdgcn_alignbyte(c.z, c.y, b);
+                    src.z = __builtin_amdgcn_alignbyte(c.w, c.z, b);
+                    src.w = __builtin_amdgcn_alignbyte(nxd, c.w, b);
+                } else {  // loaded at first (shift the bytes up) or at last (down)
+                    const u32x4 z = {0u, 0u, 0u, 0u};
+                    src = A < first ? funnel16(z, c, (uint32_t)(16 - (first - sa))) : funnel16(c, z, (uint32_t)(sa - last));
+                }
+                if (lo <= 0 && hi >= 16) {
+                    cm[u] = src;
+                } else {
+                    const uint32_t m0 = byte_mask(lo, hi, 0), m1 = byte_mask(lo, hi, 1);
+                    const uint32_t m2 = byte_mask(lo, hi, 2), m3 = byte_mask(lo, hi, 3);
+                    cm[u].x = (src.x & m0) | (cm[u].x & ~m0);
+                    cm[u].y = (src.y & m1) | (cm[u].y & ~m1);
+                    cm[u].z = (src.z & m2) | (cm[u].z & ~m2);
+                    cm[u].w = (src.w & m3) | (cm[u].w & ~m3);
+                }
+            }
+        }
+    } else if constexpr (COPY) {
         if constexpr (SHUF) {
             // the second source chunk of lane i's funnel is lane i+1's first (the group's last lane:
             // lane 0's next one), taken with all lanes of the group active
@@ -603,18 +696,37 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                 w.fip = g.fam == 4 ? g.ip_off + 10 : NO_FIELD;
                 w.fl4 = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? g.l4_off + g.fo : NO_FIELD;
                 w.fin = g.in_off ? g.in_off + 10 : NO_FIELD;
+                auto past = [&](uint32_t f) { return f != NO_FIELD && head + f + 2 > (uint32_t)WIN; };
+                w.far = past(w.fip) || past(w.fl4) || past(w.fin);
             }
         }
     }
-    if constexpr (COPY) {  // store the payload bytes of this step (all of them, summed or not)
+    // MODE_COPY: store the payload bytes of this step (all of them, summed or not).  WHOLE: store
+    // every byte of the record instead (the bytes outside the payload unchanged), so that no cache
+    // line of the batch leaves L2 partially written — a partial line costs HBM a read-modify-write
+    // (tools/probe_copy.hip: 0.818 ms with partial edge lines, 0.565 ms with whole lines) — and
+    // store the window chunks (which hold the fields) at the end of the record, fields included.
+    if constexpr (COPY) {
         const gu8 cbase = (gu8)base;
-        const int f0b = (int)w.fip, f1b = (int)w.fl4, f2b = (int)w.fin;
+        // the fields to leave out (finish writes them).  WHOLE: the window holds every field but a
+        // far one (a long IPv6 Hop-by-Hop header), so the offsets come from LDS only then
+        int f0b = (int)w.fip, f1b = (int)w.fl4, f2b = (int)w.fin;
+        if constexpr (WHOLE) {
+            f0b = f1b = f2b = -(1 << 20);
+            if (w.far) {
+                const Geom& g = *w.g;
+                f0b = g.fam == 4 ? (int)g.ip_off + 10 : -(1 << 20);
+                f1b = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? (int)(g.l4_off + g.fo) : -(1 << 20);
+                f2b = g.in_off ? (int)g.in_off + 10 : -(1 << 20);
+            }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t k = w.step * (G * U) + u * G + lane;
             const int pos = (int)(16u * k) - (int)head;
-            const int lo = (int)w.cur.p0 - pos, hi = (int)w.cur.p1 - pos;
-            if (k < w.nch && w.cur.p1 > w.cur.p0 && hi > 0 && lo < 16) {
+            const int lo = WHOLE ? -pos : (int)w.cur.p0 - pos;
+            const int hi = WHOLE ? (int)w.cur.len - pos : (int)w.cur.p1 - pos;
+            if (k < w.nch && (WHOLE ? (k >= (uint32_t)WIN_CH) : (w.cur.p1 > w.cur.p0 && hi > 0 && lo < 16))) {
                 const int f0 = f0b - pos, f1 = f1b - pos, f2 = f2b - pos;
                 const bool field = (f0 > -2 && f0 < 16) || (f1 > -2 && f1 < 16) || (f2 > -2 && f2 < 16);
                 const gu8 dst = cbase + 16u * k;
@@ -681,7 +793,33 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const uint32_t tot = group_sum<G>(s_rel);
             if (lane == 0) ((gu16)p.out16)[r] = (uint16_t)bswap16(fold32(tot));
         } else {
-            finish_gates<G, MODE, NHC>(p, GREG ? w.gr : *w.g, w.acc, rd, winb, head, w.cur.a0, r, lane);
+            finish_gates<G, MODE, NHC, decltype(rd), (COPY && WHOLE) ? WIN : 0>(
+                p, GREG ? w.gr : *w.g, w.acc, rd, winb, head, w.cur.a0, r, lane, reinterpret_cast<uint8_t*>(win));
+            if constexpr (COPY && WHOLE) {  // the window chunks, fields patched in
+                wave_lds_sync();
+                for (uint32_t k = (uint32_t)lane; k < (uint32_t)WIN_CH && k < w.nch; k += G) {
+                    const int pos = (int)(16u * k) - (int)head;
+                    const u32x4 c = win[k];
+                    const gu8 dst = (gu8)base + 16u * k;
+                    const int lo = -pos, hi = (int)w.cur.len - pos;
+                    if (lo <= 0 && hi >= 16) {
+                        *(GMEM u32x4*)dst = c;
+                    } else {
+                        const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t keep = byte_mask(lo, hi, i);
+                            if (keep == 0xffffffffu) {
+                                *(GMEM uint32_t*)(dst + 4 * i) = cw[i];
+                            } else if (keep) {
+#pragma unroll
+                                for (int j = 0; j < 4; ++j)
+                                    if (keep & (0xffu << (8 * j))) dst[4 * i + j] = (uint8_t)(cw[i] >> (8 * j));
+                            }
+                        }
+                    }
+                }
+            }
         }
     }
 
@@ -704,6 +842,8 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool LINE = VarT<VAR>::LINE;
     constexpr int CU = VarT<VAR>::CACHED_U;
     constexpr bool SHUF = VarT<VAR>::SHUF;
+    constexpr bool WHOLE = VarT<VAR>::WHOLE;
+    constexpr bool SHUF2 = VarT<VAR>::SHUF2;
     // Fixed-stride batches: no prefetch once the group has nothing left (one record per group in
     // a natural grid), measured 1-1.5 % faster (C2 verify 0.2444 -> 0.2422 ms, C4 0.2219 -> 0.2189
     // ms).  Descriptor batches keep the unconditional prefetch: there the conditional load made
@@ -733,6 +873,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     w.s1 = 0;
     w.acc = w.acc2 = 0;
     w.fip = w.fl4 = w.fin = NO_FIELD;
+    w.far = false;
 
     Regs<U, COPY> va;
     if (PF) {
@@ -746,9 +887,9 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
         }
     } else {
         while (true) {
-            load_step<G, U, NT, COPY, LINE, 0, SHUF>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
-                                                     shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF>(p, w, va, va, lane, ngroups, &win[gib][0], gib)) break;
+            load_step<G, U, NT, COPY, LINE, 0, SHUF, SHUF2>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
+                                                            shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF, WHOLE, SHUF2>(p, w, va, va, lane, ngroups, &win[gib][0], gib)) break;
         }
     }
 }
@@ -840,8 +981,8 @@ hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks
     switch (var) {
         case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
         case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);
-        case 12: return launch_copy_var<IMPLICIT, 12>(shape, p, max_blocks, s);
-        default: return launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);
+        case 8: return launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);
+        default: return launch_copy_var<IMPLICIT, 16>(shape, p, max_blocks, s);
     }
 }
 

@@ -175,13 +175,14 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
     rng = np.random.default_rng(stride + length)
     for n, base in ((1, 0), (2, 5), (33, 64), (1029, 3), (2048, 0)):
         recs, spec = _fixed_case(rng, n, length)
-        # the default, a capped grid, the prefetch variant and the lane-shuffle variants (11 / 12)
-        for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (12, 0), (12, 7), (8, 0)):
+        # the default (16), a capped grid, the prefetch variant (1), the two-load variant (8), the
+        # lane-shuffle variant (11)
+        for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (8, 0), (8, 7), (16, 0), (16, 7)):
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,
                  base=base, seed=n + variant)
 
 
-COPY_VARIANTS = [-1, 1, 8, 11, 12]
+COPY_VARIANTS = [-1, 1, 8, 11, 16]
 
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
@@ -254,7 +255,7 @@ def test_copy_emit_caps_and_rejected_records(eng):
         recs.append(r)
         spec.append((hdr, len(r) - hdr))
     for caps in [(3, 3, 3, 3, 3), (1, 2, 1, 2, 1), (0, 0, 0, 0, 0)]:
-        for variant in (-1, 11):
+        for variant in (-1, 8, 11, 16):
             _run(eng, recs, spec, caps=caps, gap_seed=8, seed=12, variant=variant)
 
 

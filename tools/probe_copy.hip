@@ -113,6 +113,43 @@ __global__ __launch_bounds__(256) void rec_copy16(const uint8_t* src, uint8_t* d
     }
 }
 
+// 8 lanes per record: each lane loads ALIGNED 16-B source chunks (the C2 source records are 16-B
+// aligned, 1472 = 92 x 16) and stores each one UNALIGNED at its destination (dst + r*1500 + 28 +
+// 16k, misaligned by (r*1500 + 28) % 16): no funnel shift at all.  FULL: the 28 header bytes are
+// written too (two overlapping unaligned 16-B stores), so no line is left partially written.
+template <bool FULL>
+__global__ __launch_bounds__(256) void rec_copy_unal(const uint8_t* src, uint8_t* dst, uint64_t n) {
+    const int lane = threadIdx.x & 7;
+    const uint64_t r = (uint64_t)blockIdx.x * 32 + threadIdx.x / 8;
+    if (r >= n) return;
+    const uint64_t s0 = (uint64_t)src + r * 1472, d0 = (uint64_t)dst + r * 1500;
+#pragma unroll
+    for (int k0 = 0; k0 < 96; k0 += 32) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + u * 8 + lane;
+            v[u] = *(const GMEM u32x4*)(s0 + 16ull * (k < 92 ? k : 91));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + u * 8 + lane;
+            if (k < 92) *(GMEM u32x4*)(d0 + 28 + 16ull * k) = v[u];
+        }
+    }
+    if (FULL && lane < 2) {
+        const u32x4 h = {0x45000000u, 0x01020304u, 0x05060708u, 0x090a0b0cu};
+        *(GMEM u32x4*)(d0 + 12 * lane) = h;
+    }
+}
+
+__global__ void check_unal(const uint8_t* src, const uint8_t* dst, uint64_t n, uint32_t* bad) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    for (int i = 0; i < 1472; ++i)
+        if (dst[r * 1500 + 28 + i] != src[r * 1472 + i]) { atomicAdd(bad, 1u); return; }
+}
+
 int main() {
     const uint64_t bytes = 1500ull << 20;
     uint8_t *a, *b;
@@ -149,6 +186,19 @@ int main() {
     timeit("rec_copy_full 1500 B (all bytes)", [&] { hipLaunchKernelGGL(rec_copy_full, dim3(256 * 8), dim3(256), 0, 0, a, b, n); });
     timeit("rec_copy16 own lines (whole lines)", [&] { hipLaunchKernelGGL(rec_copy16<true>, dim3(n / 32), dim3(256), 0, 0, a, b, n); });
     timeit("rec_copy16 [28,1500) (partial edges)", [&] { hipLaunchKernelGGL(rec_copy16<false>, dim3(n / 32), dim3(256), 0, 0, a, b, n); });
+    timeit("rec_copy_unal [28,1500) unaligned 16-B stores", [&] { hipLaunchKernelGGL(rec_copy_unal<false>, dim3(n / 32), dim3(256), 0, 0, a, b, n); });
+    timeit("rec_copy_unal all bytes (unaligned)", [&] { hipLaunchKernelGGL(rec_copy_unal<true>, dim3(n / 32), dim3(256), 0, 0, a, b, n); });
+    {  // the unaligned stores land where they should (a source with distinct bytes)
+        uint8_t* h = (uint8_t*)malloc(n * 1472);
+        for (uint64_t i = 0; i < n * 1472; ++i) h[i] = (uint8_t)(i * 2654435761u >> 13);
+        CK(hipMemcpy(a, h, n * 1472, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(rec_copy_unal<false>, dim3(n / 32), dim3(256), 0, 0, a, b, n);
+        uint32_t* bad; CK(hipMalloc(&bad, 4)); CK(hipMemset(bad, 0, 4));
+        hipLaunchKernelGGL(check_unal, dim3(n / 256), dim3(256), 0, 0, a, b, n, bad);
+        uint32_t hb = 0; CK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
+        printf("rec_copy_unal check: %u of %llu records differ\n", hb, (unsigned long long)n);
+        free(h);
+    }
     CK(hipGetLastError());
     return 0;
 }
