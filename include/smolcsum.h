@@ -200,7 +200,9 @@ typedef struct {
  * smol_csum_batch_emit, including when the copied range covers a checksum field (the emitted
  * field wins).  A record whose copy range does not fit (dst_offset + len > record length) is
  * left untouched and reported SMOL_ST_MALFORMED.  `d_copy` is a 16-byte-aligned device array of
- * n entries; the source must not overlap the batch buffer. */
+ * n entries; the source must not overlap the batch buffer, and records must not overlap one another
+ * (the kernel rewrites every byte of a record — the bytes outside its copy range with their own
+ * values — so that whole cache lines leave L2). */
 int smol_csum_batch_copy_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                               const uint8_t* d_src, const smol_csum_copy_t* d_copy,
                               const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);

@@ -16,7 +16,7 @@ step() {  # step <name> <seconds> <cmd...>: stop the whole script on the first f
 step tests 900 python -m pytest tests -m gpu -x -q
 tail -3 $O/tests.log
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-for c in c2 c3 c4; do
+for c in ${BENCH_CONFIGS:-c2 c3 c4}; do
     step bench_$c 400 python bench.py --config $c --probe
     tail -1 $O/bench_$c.log
 done
