@@ -24,7 +24,13 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPT
 
 @pytest.fixture(scope="module")
 def built():
-    subprocess.run(["make", "-s", "-C", CPP, "sanitize"], check=True, timeout=600)
+    # one build at a time: under pytest-xdist every worker runs this fixture, and a make that
+    # relinks a binary while another worker executes it fails that worker's test
+    import fcntl
+
+    with open(os.path.join(CPP, ".sanitize.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", CPP, "sanitize"], check=True, timeout=600)
     return CPP
 
 
