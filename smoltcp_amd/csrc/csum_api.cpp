@@ -163,7 +163,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         // default: variant 16 (dword-aligned source loads, one dword from the next lane, every record
         // byte written): C2copy 0.860 -> 0.800 ms against variant 8 (tools/exp_copy.py, MI355X)
         const int cv = ctx->variant;
-        hipError_t e = launch_csum(MODE_COPY, shape, (cv == 1 || cv == 8 || cv == 11) ? cv : 16, p, ctx->max_blocks, s);
+        hipError_t e = launch_csum(MODE_COPY, shape, (cv == 1 || cv == 8 || cv == 11 || cv == 17 || cv == 18) ? cv : 16, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
     }
@@ -377,7 +377,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 16) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 18) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

@@ -1,0 +1,308 @@
+// Fused payload copy + emit, second design (variant 17): the walk kernel's MODE_COPY split by chunk
+// class, so that the bulk of a record costs what a copy costs.
+//
+// TcpRepr::emit / UdpRepr::emit copy the payload into the packet and then fill the checksum
+// (src/wire/tcp.rs:1087-1095, src/wire/udp.rs:300-308).  The result here is bit-identical to a
+// memcpy of every payload followed by smol_csum_batch_emit, as in MODE_COPY of csum_walk.h, whose
+// helpers (rec_at, parse_geometry, finish_gates) this kernel shares.
+//
+// A group of G lanes owns a record.  Its 16-B destination chunks fall into two classes:
+// * BODY chunks lie past the 128-B header window and entirely inside the copy range.  A lane reads
+//   the 16 source bytes from the chunk's first source byte rounded down to 4 (one dwordx4 load) and
+//   the dword after them (one dword load), shifts them to the destination alignment with four
+//   v_alignbyte, sums them and stores them: no destination load, no mask, no neighbour exchange.
+//   That loop is unrolled U deep, all loads issued first.
+// * GENERIC chunks — the window (the first 128 B of the chunk grid, which hold the headers the gates
+//   parse) and any chunk past it that holds bytes outside the copy range (normally just the
+//   record's last chunk) — are built from the destination chunk and two aligned source chunks with
+//   byte masks.  The window and the first few other generic chunks are loaded in ONE round before
+//   the parse, so a C2copy record takes one round trip for its headers and tail, then
+//   ceil(body / (G * U)) for its body.
+// Every byte of the record is written (bytes outside the copy range with their own values, so no
+// line is left half-written by this kernel); the window chunks go out last from LDS, with the
+// fields finish_gates patched in.  A field past the window (behind a long IPv6 Hop-by-Hop header)
+// is left out of the chunk stores and written by finish_gates.
+#include "csum_walk.h"
+
+namespace smolcsum {
+
+namespace copy2 {
+
+// Store the bytes [lo, hi) of chunk c (chunk-relative) at dst, leaving out any byte of the fields
+// starting at chunk-relative f0 / f1 / f2 (2 bytes each).
+__device__ __forceinline__ void store_part(gu8 dst, const u32x4& c, int lo, int hi, int f0, int f1, int f2) {
+    const bool field = (f0 > -2 && f0 < 16) || (f1 > -2 && f1 < 16) || (f2 > -2 && f2 < 16);
+    if (lo <= 0 && hi >= 16 && !field) {
+        *(GMEM u32x4*)dst = c;
+        return;
+    }
+    const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t keep = byte_mask(lo, hi, i);
+        keep &= ~byte_mask(f0, f0 + 2, i);
+        keep &= ~byte_mask(f1, f1 + 2, i);
+        keep &= ~byte_mask(f2, f2 + 2, i);
+        if (keep == 0xffffffffu) {
+            *(GMEM uint32_t*)(dst + 4 * i) = cw[i];
+        } else if (keep) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (keep & (0xffu << (8 * j))) dst[4 * i + j] = (uint8_t)(cw[i] >> (8 * j));
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t sum_chunk(const u32x4& c, int pos, int s1, uint32_t acc) {
+    // aligned-word sum of the chunk's bytes inside the record span [0, s1) (pos: chunk start
+    // relative to the record start)
+    if (pos >= s1 || pos + 16 <= 0) return acc;
+    if (pos < 0 || pos + 16 > s1) return sum_masked_words(c, -pos, s1 - pos, acc);
+    return add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, acc))));
+}
+
+constexpr int WIN = 128;  // the header window: 16-B grid, Grid<false>
+constexpr int WIN_CH = WIN / 16;
+constexpr int NOF = -(1 << 20);  // "no field" for store_part
+
+}  // namespace copy2
+
+template <int G, int U, bool IMPLICIT, bool NTS>
+__global__ __launch_bounds__(256) void copy_kernel(KParams p) {
+    using namespace copy2;
+    constexpr int GPB = 256 / G;
+    // generic slots loaded before the parse: the window plus at least 8 chunks past it
+    constexpr int UW = (WIN_CH + 8 + G - 1) / G;
+    constexpr uint32_t NEX = (uint32_t)(UW * G - WIN_CH);  // generic chunks past the window in that round
+    static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
+    __shared__ u32x4 win[GPB][WIN_CH];
+    __shared__ Geom geo[GPB];
+
+    const int lane = (int)(threadIdx.x % G);
+    const int gib = (int)(threadIdx.x / G);
+    const uint64_t ngroups = (uint64_t)gridDim.x * GPB;
+    u32x4* wn = &win[gib][0];
+    const uint8_t* winb = reinterpret_cast<const uint8_t*>(wn);
+    const uint64_t dummy = (uint64_t)p.dummy;
+
+    for (uint64_t r = (uint64_t)blockIdx.x * GPB + gib; r < p.n; r += ngroups) {
+        const RecRef rr = rec_at<IMPLICIT, true>(p, r);
+        if (rr.kind & KIND_BAD_COPY) {  // the copy range does not fit: record left untouched
+            if (lane == 0 && p.status) ((gu8)p.status)[r] = (uint8_t)SMOL_ST_MALFORMED;
+            continue;
+        }
+        const uint64_t base = rr.a0 & ~15ull;
+        const uint32_t head = (uint32_t)(rr.a0 - base);
+        const uint32_t nch = n_chunks<false>(rr);
+        const bool pay = rr.p1 > rr.p0;
+        const uint64_t sk = rr.sb - head;  // source address of grid byte 0 (payload bytes only)
+        const uint64_t first = (rr.sb + rr.p0) & ~15ull, last = (rr.sb + rr.p1 - 1) & ~15ull;
+        // body chunks [kb0, kb1): past the window, entirely inside the copy range
+        uint32_t kb0 = pay ? (head + rr.p0 + 15) >> 4 : nch;
+        kb0 = kb0 > (uint32_t)WIN_CH ? kb0 : (uint32_t)WIN_CH;
+        uint32_t kb1 = pay ? (head + rr.p1) >> 4 : 0u;
+        kb1 = kb1 < nch ? kb1 : nch;
+        kb1 = kb1 > kb0 ? kb1 : kb0;
+        // generic chunks past the window: [WIN_CH, min(kb0, nch)) then [kb1, nch)
+        const uint32_t e1 = kb0 < nch ? kb0 : nch;
+        const uint32_t n1 = e1 > (uint32_t)WIN_CH ? e1 - WIN_CH : 0u;
+        const uint32_t n2 = nch > kb1 ? nch - kb1 : 0u;
+        const uint32_t ne = n1 + n2;
+        auto gen_k = [&](uint32_t e) -> uint32_t { return e < n1 ? WIN_CH + e : kb1 + (e - n1); };
+
+        // a generic chunk: the destination chunk (unless it is all payload) and the two aligned
+        // source chunks under its payload bytes (clamped into the source range's aligned chunks:
+        // bytes outside the range are masked anyway, and no load leaves the range)
+        auto gen_load = [&](uint32_t k, bool in, u32x4& d, u32x4& c0, u32x4& c1) {
+            const int pos = (int)(16u * k) - (int)head;
+            const int lo = (int)rr.p0 - pos, hi = (int)rr.p1 - pos;
+            const bool full = lo <= 0 && hi >= 16;
+            const bool any = pay && lo < 16 && hi > 0;
+            d = ld16<false>((gcv4)(in && !(pay && full) ? base + 16ull * k : dummy));
+            const uint64_t sA = (sk + 16ull * k) & ~15ull;
+            const uint64_t a0 = sA < first ? first : sA > last ? last : sA;
+            const uint64_t a1 = sA + 16 < first ? first : sA + 16 > last ? last : sA + 16;
+            c0 = ld16<false>((gcv4)(in && any ? a0 : dummy));
+            c1 = ld16<false>((gcv4)(in && any && (sk & 15u) ? a1 : dummy));
+        };
+        auto gen_merge = [&](uint32_t k, const u32x4& d, const u32x4& c0, const u32x4& c1) -> u32x4 {
+            const int pos = (int)(16u * k) - (int)head;
+            const int lo = (int)rr.p0 - pos, hi = (int)rr.p1 - pos;
+            if (!(pay && lo < 16 && hi > 0)) return d;
+            const u32x4 s = funnel16(c0, c1, (uint32_t)(sk & 15u));
+            if (lo <= 0 && hi >= 16) return s;
+            u32x4 m;
+            const uint32_t m0 = byte_mask(lo, hi, 0), m1 = byte_mask(lo, hi, 1);
+            const uint32_t m2 = byte_mask(lo, hi, 2), m3 = byte_mask(lo, hi, 3);
+            m.x = (s.x & m0) | (d.x & ~m0);
+            m.y = (s.y & m1) | (d.y & ~m1);
+            m.z = (s.z & m2) | (d.z & ~m2);
+            m.w = (s.w & m3) | (d.w & ~m3);
+            return m;
+        };
+
+        // ---- round 1: the window and the first generic chunks past it ----
+        u32x4 gm[UW];
+        {
+            u32x4 d[UW], c0[UW], c1[UW];
+#pragma unroll
+            for (int u = 0; u < UW; ++u) {
+                const uint32_t j = (uint32_t)(u * G + lane);
+                const bool w = j < (uint32_t)WIN_CH;
+                const uint32_t k = w ? j : gen_k(j - WIN_CH);
+                const bool in = w ? j < nch : j - WIN_CH < ne;
+                gen_load(k, in, d[u], c0[u], c1[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < UW; ++u) {
+                const uint32_t j = (uint32_t)(u * G + lane);
+                const bool w = j < (uint32_t)WIN_CH;
+                const uint32_t k = w ? j : gen_k(j - WIN_CH);
+                gm[u] = gen_merge(k, d[u], c0[u], c1[u]);
+                if (w && j < nch) wn[j] = gm[u];
+            }
+        }
+        wave_lds_sync();
+        // record byte o: the LDS window, else global memory (payload bytes from the source)
+        auto rd = [&](uint32_t o) -> uint32_t {
+            const uint32_t x = head + o;
+            if (x < (uint32_t)WIN) return (uint32_t)winb[x];
+            if (o >= rr.p0 && o < rr.p1) return ld_byte_sync(rr.sb + o);
+            return ld_byte_sync(rr.a0 + o);
+        };
+        {
+            const Geom g0 = parse_geometry<false>(rd, rr.len, rr.kind, true);
+            if (lane == 0) geo[gib] = g0;
+        }
+        wave_lds_sync();
+        const Geom& g = geo[gib];
+        const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
+        const int s1 = l4 ? (int)g.span_end : 0;
+        // fields past the window stay out of the chunk stores (finish_gates writes them)
+        int f0b = NOF, f1b = NOF, f2b = NOF;
+        {
+            const uint32_t fip = g.fam == 4 ? g.ip_off + 10 : NO_FIELD;
+            const uint32_t fl4 = l4 ? g.l4_off + g.fo : NO_FIELD;
+            const uint32_t fin = g.in_off ? g.in_off + 10 : NO_FIELD;
+            auto past = [&](uint32_t f) { return f != NO_FIELD && head + f + 2 > (uint32_t)WIN; };
+            if (past(fip) || past(fl4) || past(fin)) {
+                f0b = fip != NO_FIELD ? (int)fip : NOF;
+                f1b = fl4 != NO_FIELD ? (int)fl4 : NOF;
+                f2b = fin != NO_FIELD ? (int)fin : NOF;
+            }
+        }
+        const bool far = f0b != NOF || f1b != NOF || f2b != NOF;
+        const int len = (int)rr.len;
+
+        // ---- sum round 1; store its chunks past the window ----
+        uint32_t acc = 0;
+#pragma unroll
+        for (int u = 0; u < UW; ++u) {
+            const uint32_t j = (uint32_t)(u * G + lane);
+            const bool w = j < (uint32_t)WIN_CH;
+            const uint32_t k = w ? j : gen_k(j - WIN_CH);
+            const bool in = w ? j < nch : j - WIN_CH < ne;
+            if (in) {
+                const int pos = (int)(16u * k) - (int)head;
+                acc = sum_chunk(gm[u], pos, s1, acc);
+                if (!w) store_part((gu8)base + 16u * k, gm[u], -pos, len - pos, f0b - pos, f1b - pos, f2b - pos);
+            }
+        }
+        // generic chunks beyond round 1 (a copy range that starts or ends far from the record's edges)
+        for (uint32_t e0 = NEX; e0 < ne; e0 += G) {
+            const uint32_t e = e0 + (uint32_t)lane;
+            const bool in = e < ne;
+            const uint32_t k = gen_k(in ? e : 0u);
+            u32x4 d, c0, c1;
+            gen_load(k, in, d, c0, c1);
+            const u32x4 m = gen_merge(k, d, c0, c1);
+            if (in) {
+                const int pos = (int)(16u * k) - (int)head;
+                acc = sum_chunk(m, pos, s1, acc);
+                store_part((gu8)base + 16u * k, m, -pos, len - pos, f0b - pos, f1b - pos, f2b - pos);
+            }
+        }
+
+        // ---- body: copy + sum, U chunks per lane per round ----
+        const uint32_t nb = kb1 - kb0;
+        const uint64_t skA = sk & ~3ull;
+        const uint32_t b = (uint32_t)(sk & 3u);
+        for (uint32_t i0 = 0; i0 < nb; i0 += (uint32_t)(G * U)) {
+            u32x4 lo[U];
+            uint32_t hi[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = i0 + (uint32_t)(u * G + lane);
+                const bool in = i < nb;
+                const uint64_t A = skA + 16ull * (kb0 + i);
+                lo[u] = ld16<NTS>((gcv4)(in ? A : dummy));
+                // the dword after them holds the chunk's last b bytes (none when b == 0: that dword
+                // may lie past the source range)
+                hi[u] = *(const GMEM uint32_t*)(in && b ? A + 16 : dummy);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = i0 + (uint32_t)(u * G + lane);
+                if (i < nb) {
+                    const uint32_t k = kb0 + i;
+                    u32x4 m;
+                    m.x = __builtin_amdgcn_alignbyte(lo[u].y, lo[u].x, b);
+                    m.y = __builtin_amdgcn_alignbyte(lo[u].z, lo[u].y, b);
+                    m.z = __builtin_amdgcn_alignbyte(lo[u].w, lo[u].z, b);
+                    m.w = __builtin_amdgcn_alignbyte(hi[u], lo[u].w, b);
+                    const int pos = (int)(16u * k) - (int)head;
+                    acc = sum_chunk(m, pos, s1, acc);
+                    const gu8 dst = (gu8)base + 16u * k;
+                    if (!far) *(GMEM u32x4*)dst = m;
+                    else store_part(dst, m, 0, 16, f0b - pos, f1b - pos, f2b - pos);
+                }
+            }
+        }
+
+        // ---- finish: gates, fields into the window (or past it), then the window chunks ----
+        finish_gates<G, MODE_COPY, false, decltype(rd), WIN>(p, g, acc, rd, winb, head, rr.a0, r, lane,
+                                                              reinterpret_cast<uint8_t*>(wn));
+        wave_lds_sync();
+        for (uint32_t k = (uint32_t)lane; k < (uint32_t)WIN_CH && k < nch; k += G) {
+            const int pos = (int)(16u * k) - (int)head;
+            store_part((gu8)base + 16u * k, wn[k], -pos, len - pos, NOF, NOF, NOF);
+        }
+        wave_lds_sync();  // the window is rewritten by the group's next record
+    }
+}
+
+template <bool IMPLICIT, int G, int U, bool NTS = false>
+hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    constexpr uint32_t GPB = 256 / G;
+    const uint64_t want = (p.n + GPB - 1) / GPB;
+    const uint32_t blocks = grid_blocks(want, max_blocks);
+    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, NTS>), dim3(blocks), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+// Shapes: 8 lanes x 6 body chunks per round (the default: a C2copy body of 85 chunks in two rounds),
+// 8 x 4, 16 x 3, 32 x 2, 64 x 2.
+template <bool IMPLICIT, bool NTS>
+hipError_t launch_copy2(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    switch (shape) {
+        case CFG_G8U6: return launch_copy2_one<IMPLICIT, 8, 6, NTS>(p, max_blocks, s);
+        case CFG_G8U7: return launch_copy2_one<IMPLICIT, 8, 4, NTS>(p, max_blocks, s);
+        case CFG_G16U4: return launch_copy2_one<IMPLICIT, 16, 4, NTS>(p, max_blocks, s);
+        case CFG_G16U6: return launch_copy2_one<IMPLICIT, 16, 6, NTS>(p, max_blocks, s);
+        case CFG_G32U3: return launch_copy2_one<IMPLICIT, 32, 3, NTS>(p, max_blocks, s);
+        case CFG_G32U4: return launch_copy2_one<IMPLICIT, 32, 2, NTS>(p, max_blocks, s);
+        case CFG_G64U2:
+        case CFG_G64U4: return launch_copy2_one<IMPLICIT, 64, 2, NTS>(p, max_blocks, s);
+        default: return launch_copy2_one<IMPLICIT, 16, 3, NTS>(p, max_blocks, s);
+    }
+}
+
+hipError_t launch_copy_v17(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    if (var == 18)
+        return p.desc == nullptr ? launch_copy2<true, true>(shape, p, max_blocks, s)
+                                 : launch_copy2<false, true>(shape, p, max_blocks, s);
+    return p.desc == nullptr ? launch_copy2<true, false>(shape, p, max_blocks, s)
+                             : launch_copy2<false, false>(shape, p, max_blocks, s);
+}
+
+}  // namespace smolcsum

@@ -547,7 +547,9 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib) {
     constexpr bool COPY = MODE == MODE_COPY;
-    constexpr bool GREG = MODE == MODE_EMIT;  // where the record geometry lives (Walk::g / Walk::gr)
+    // where the record geometry lives (Walk::g / Walk::gr): registers for emit with the register
+    // prefetch, LDS otherwise
+    constexpr bool GREG = MODE == MODE_EMIT && PF;
     constexpr int WIN = Grid<LINE>::WIN;
     constexpr int WIN_CH = Grid<LINE>::WIN_CH;
     static_assert(G * U >= WIN_CH, "step 0 must cover the LDS window");
@@ -976,9 +978,14 @@ hipError_t launch_copy_var(int shape, const KParams& p, uint32_t max_blocks, hip
     }
 }
 
+// variant 17: the class-split copy-emit kernel (csum_copy.hip)
+hipError_t launch_copy_v17(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s);
+
 template <bool IMPLICIT>
 hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (var) {
+        case 17:
+        case 18: return launch_copy_v17(shape, var, p, max_blocks, s);
         case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
         case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);
         case 8: return launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);

@@ -177,16 +177,17 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
         recs, spec = _fixed_case(rng, n, length)
         # the default (16), a capped grid, the prefetch variant (1), the two-load variant (8), the
         # lane-shuffle variant (11)
-        for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (8, 0), (8, 7), (16, 0), (16, 7)):
+        for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (8, 0), (8, 7), (16, 0), (16, 7), (17, 0),
+                               (17, 7)):
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,
                  base=base, seed=n + variant)
 
 
-COPY_VARIANTS = [-1, 1, 8, 11, 16]
+COPY_VARIANTS = [-1, 1, 8, 11, 16, 17]
 
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
-@pytest.mark.parametrize("shape", [-1, 0, 1, 3, 5])
+@pytest.mark.parametrize("shape", [-1, 0, 1, 3, 5, 7])
 def test_copy_emit_mixed_packed(eng, shape, variant):
     rng = np.random.default_rng(10 + shape)
     recs, spec = [], []
@@ -255,7 +256,7 @@ def test_copy_emit_caps_and_rejected_records(eng):
         recs.append(r)
         spec.append((hdr, len(r) - hdr))
     for caps in [(3, 3, 3, 3, 3), (1, 2, 1, 2, 1), (0, 0, 0, 0, 0)]:
-        for variant in (-1, 8, 11, 16):
+        for variant in (-1, 8, 11, 16, 17):
             _run(eng, recs, spec, caps=caps, gap_seed=8, seed=12, variant=variant)
 
 
@@ -266,3 +267,37 @@ def test_copy_emit_errors(eng):
     with pytest.raises(Exception):
         eng.copy_emit(d, b, d, cp[1:17])  # copies array not 16-byte aligned
     eng.copy_emit(d, E.Batch.fixed(0, 64, 64, E.KIND_IP), d, cp)  # empty batch: no-op
+
+
+@pytest.mark.parametrize("variant", COPY_VARIANTS)
+def test_copy_emit_far_fields(eng, variant):
+    """IPv6 records whose Hop-by-Hop header pushes the TCP / UDP checksum field past the 128-B
+    header window (or across its edge): the field must still be the emitted value, whether the copy
+    range covers it or not, at every record alignment."""
+    rng = np.random.default_rng(21)
+    recs, spec = [], []
+    for i in range(600):
+        units = int(rng.integers(6, 40))  # 56 .. 320 B of Hop-by-Hop header
+        pay = P.rand_bytes(rng, int(rng.integers(0, 900)))
+        if i % 2:
+            l4 = P.udp(7 + i, 9, pay)
+            nh, fo = 17, 6
+        else:
+            l4 = P.tcp(7 + i, 9, pay, doff=5 + i % 4)
+            nh, fo = 6, 16
+        hb = P.hbh(nh, units, rng)
+        r = P.ipv6(V6A, V6B, 0, hb + l4)
+        l4_off = 40 + len(hb)
+        recs.append(r)
+        m = i % 4
+        if m == 0:
+            spec.append((l4_off + (8 if nh == 17 else 4 * (5 + i % 4)), len(pay)))  # the payload
+        elif m == 1:
+            spec.append((l4_off + fo - 3, min(40, len(r) - (l4_off + fo - 3))))  # over the field
+        elif m == 2:
+            spec.append((40, len(r) - 40))  # everything after the IPv6 header
+        else:
+            spec.append((int(rng.integers(0, len(r))), 0))
+    for shape in (-1, 1, 3):
+        st, got, _, _ = _run(eng, recs, spec, gap_seed=13, seed=14 + shape, variant=variant, shape=shape)
+        assert (st & E.ST_MALFORMED).sum() == 0
