@@ -160,10 +160,13 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, has_desc, line_grid(variant), variant);
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
-        // default: variant 16 (dword-aligned source loads, one dword from the next lane, every record
-        // byte written): C2copy 0.860 -> 0.800 ms against variant 8 (tools/exp_copy.py, MI355X)
+        // default: variant 17 (csum_copy.hip: body chunks = one source load + shift + sum + store,
+        // window and edge chunks generic) at 16 x 3: C2copy 0.798 ms (variant 16, 8 x 3) -> 0.709-0.743
+        // ms (tools/exp_copy.py, MI355X, three boxes).  Variants 1 / 8 / 11 / 16 stay selectable.
         const int cv = ctx->variant;
-        hipError_t e = launch_csum(MODE_COPY, shape, (cv == 1 || cv == 8 || cv == 11 || cv == 17 || cv == 18) ? cv : 16, p, ctx->max_blocks, s);
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? cv : 17;
+        const int cshape = ctx->shape >= 0 ? ctx->shape : (var == 17 ? (int)CFG_G16U3 : shape);
+        hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
     }
@@ -377,7 +380,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 18) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 17) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }
@@ -412,6 +415,10 @@ int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
 
 const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int has_desc) {
     if (!ctx || op < MODE_DATA || op > MODE_COPY) return "";
+    if (op == MODE_COPY) {
+        const int cv = ctx->variant;
+        return (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? "csum_kernel" : "copy_kernel";
+    }
     const int v = ctx->variant >= 0 ? ctx->variant : auto_variant(op, has_desc != 0);
     const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY);
     return tile ? "csum_tile_kernel" : "csum_kernel";

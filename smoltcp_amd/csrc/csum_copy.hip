@@ -67,7 +67,7 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 
 }  // namespace copy2
 
-template <int G, int U, bool IMPLICIT, bool NTS>
+template <int G, int U, bool IMPLICIT>
 __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
     constexpr int GPB = 256 / G;
@@ -140,6 +140,25 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             m.w = (s.w & m3) | (d.w & ~m3);
             return m;
         };
+
+        // body chunks: U per lane per round; their loads need only the copy range, not the parse
+        const uint32_t nb = kb1 - kb0;
+        const uint64_t skA = sk & ~3ull;
+        const uint32_t b = (uint32_t)(sk & 3u);
+        auto body_load = [&](uint32_t i0, u32x4* lo, uint32_t* hi) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = i0 + (uint32_t)(u * G + lane);
+                const bool in = i < nb;
+                const uint64_t A = skA + 16ull * (kb0 + i);
+                lo[u] = ld16<false>((gcv4)(in ? A : dummy));
+                // the dword after them holds the chunk's last b bytes (none when b == 0: that dword
+                // may lie past the source range)
+                hi[u] = *(const GMEM uint32_t*)(in && b ? A + 16 : dummy);
+            }
+        };
+        u32x4 blo[U];
+        uint32_t bhi[U];
 
         // ---- round 1: the window and the first generic chunks past it ----
         u32x4 gm[UW];
@@ -223,33 +242,19 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             }
         }
 
-        // ---- body: copy + sum, U chunks per lane per round ----
-        const uint32_t nb = kb1 - kb0;
-        const uint64_t skA = sk & ~3ull;
-        const uint32_t b = (uint32_t)(sk & 3u);
+        // ---- body: copy + sum ----
         for (uint32_t i0 = 0; i0 < nb; i0 += (uint32_t)(G * U)) {
-            u32x4 lo[U];
-            uint32_t hi[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t i = i0 + (uint32_t)(u * G + lane);
-                const bool in = i < nb;
-                const uint64_t A = skA + 16ull * (kb0 + i);
-                lo[u] = ld16<NTS>((gcv4)(in ? A : dummy));
-                // the dword after them holds the chunk's last b bytes (none when b == 0: that dword
-                // may lie past the source range)
-                hi[u] = *(const GMEM uint32_t*)(in && b ? A + 16 : dummy);
-            }
+            body_load(i0, blo, bhi);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t i = i0 + (uint32_t)(u * G + lane);
                 if (i < nb) {
                     const uint32_t k = kb0 + i;
                     u32x4 m;
-                    m.x = __builtin_amdgcn_alignbyte(lo[u].y, lo[u].x, b);
-                    m.y = __builtin_amdgcn_alignbyte(lo[u].z, lo[u].y, b);
-                    m.z = __builtin_amdgcn_alignbyte(lo[u].w, lo[u].z, b);
-                    m.w = __builtin_amdgcn_alignbyte(hi[u], lo[u].w, b);
+                    m.x = __builtin_amdgcn_alignbyte(blo[u].y, blo[u].x, b);
+                    m.y = __builtin_amdgcn_alignbyte(blo[u].z, blo[u].y, b);
+                    m.z = __builtin_amdgcn_alignbyte(blo[u].w, blo[u].z, b);
+                    m.w = __builtin_amdgcn_alignbyte(bhi[u], blo[u].w, b);
                     const int pos = (int)(16u * k) - (int)head;
                     acc = sum_chunk(m, pos, s1, acc);
                     const gu8 dst = (gu8)base + 16u * k;
@@ -271,38 +276,35 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     }
 }
 
-template <bool IMPLICIT, int G, int U, bool NTS = false>
+template <bool IMPLICIT, int G, int U>
 hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, NTS>), dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
-// Shapes: 8 lanes x 6 body chunks per round (the default: a C2copy body of 85 chunks in two rounds),
-// 8 x 4, 16 x 3, 32 x 2, 64 x 2.
-template <bool IMPLICIT, bool NTS>
+// Shapes (lanes per record x body chunks per lane per round).  16 x 3, the default, takes a C2copy
+// body (85 chunks) in two rounds: 0.7085-0.743 ms on MI355X against 0.761-0.842 for 8 x 6, 0.805 for
+// 16 x 4, 0.85 for 16 x 6 and 1.05-1.08 for 32 x 3 (tools/exp_copy.py).
+template <bool IMPLICIT>
 hipError_t launch_copy2(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (shape) {
-        case CFG_G8U6: return launch_copy2_one<IMPLICIT, 8, 6, NTS>(p, max_blocks, s);
-        case CFG_G8U7: return launch_copy2_one<IMPLICIT, 8, 4, NTS>(p, max_blocks, s);
-        case CFG_G16U4: return launch_copy2_one<IMPLICIT, 16, 4, NTS>(p, max_blocks, s);
-        case CFG_G16U6: return launch_copy2_one<IMPLICIT, 16, 6, NTS>(p, max_blocks, s);
-        case CFG_G32U3: return launch_copy2_one<IMPLICIT, 32, 3, NTS>(p, max_blocks, s);
-        case CFG_G32U4: return launch_copy2_one<IMPLICIT, 32, 2, NTS>(p, max_blocks, s);
+        case CFG_G8U6: return launch_copy2_one<IMPLICIT, 8, 6>(p, max_blocks, s);
+        case CFG_G8U7: return launch_copy2_one<IMPLICIT, 8, 4>(p, max_blocks, s);
+        case CFG_G16U4: return launch_copy2_one<IMPLICIT, 16, 4>(p, max_blocks, s);
+        case CFG_G16U6: return launch_copy2_one<IMPLICIT, 16, 6>(p, max_blocks, s);
+        case CFG_G32U3: return launch_copy2_one<IMPLICIT, 32, 3>(p, max_blocks, s);
+        case CFG_G32U4: return launch_copy2_one<IMPLICIT, 32, 2>(p, max_blocks, s);
         case CFG_G64U2:
-        case CFG_G64U4: return launch_copy2_one<IMPLICIT, 64, 2, NTS>(p, max_blocks, s);
-        default: return launch_copy2_one<IMPLICIT, 16, 3, NTS>(p, max_blocks, s);
+        case CFG_G64U4: return launch_copy2_one<IMPLICIT, 64, 2>(p, max_blocks, s);
+        default: return launch_copy2_one<IMPLICIT, 16, 3>(p, max_blocks, s);
     }
 }
 
-hipError_t launch_copy_v17(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    if (var == 18)
-        return p.desc == nullptr ? launch_copy2<true, true>(shape, p, max_blocks, s)
-                                 : launch_copy2<false, true>(shape, p, max_blocks, s);
-    return p.desc == nullptr ? launch_copy2<true, false>(shape, p, max_blocks, s)
-                             : launch_copy2<false, false>(shape, p, max_blocks, s);
+hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    return p.desc == nullptr ? launch_copy2<true>(shape, p, max_blocks, s) : launch_copy2<false>(shape, p, max_blocks, s);
 }
 
 }  // namespace smolcsum

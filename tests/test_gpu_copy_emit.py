@@ -175,8 +175,8 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
     rng = np.random.default_rng(stride + length)
     for n, base in ((1, 0), (2, 5), (33, 64), (1029, 3), (2048, 0)):
         recs, spec = _fixed_case(rng, n, length)
-        # the default (16), a capped grid, the prefetch variant (1), the two-load variant (8), the
-        # lane-shuffle variant (11)
+        # the default (17), a capped grid, the prefetch variant (1), the two-load variant (8), the
+        # lane-shuffle variants (11, 16)
         for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (8, 0), (8, 7), (16, 0), (16, 7), (17, 0),
                                (17, 7)):
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,

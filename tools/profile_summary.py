@@ -35,6 +35,8 @@ def _find(d, pattern):
 
 def kernel_role(name: str):
     """'emit' / 'verify' / 'data' for the checksum kernels, else None."""
+    if re.search(r"copy_kernel<", name):  # csum_copy.hip: <G, U, IMPLICIT>, copy-emit only
+        return "copy_emit"
     m = re.search(r"(csum_kernel|csum_tile_kernel)<([^>]*)>", name)
     if not m:
         return None
