@@ -161,11 +161,12 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
         // default: variant 17 (csum_copy.hip: body chunks = one source load + shift + sum + store,
-        // window and edge chunks generic) at 16 x 3: C2copy 0.798 ms (variant 16, 8 x 3) -> 0.709-0.743
-        // ms (tools/exp_copy.py, MI355X, three boxes).  Variants 1 / 8 / 11 / 16 stay selectable.
+        // window and edge chunks generic) at 16 x 4 with two round-1 slots per lane: C2copy 0.772-0.853
+        // ms (variant 16) -> 0.709-0.760 ms (16 x 3) -> 0.738 ms (16 x 4, same box as 0.760)
+        // (tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 stay selectable.
         const int cv = ctx->variant;
         const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? cv : 17;
-        const int cshape = ctx->shape >= 0 ? ctx->shape : (var == 17 ? (int)CFG_G16U3 : shape);
+        const int cshape = ctx->shape >= 0 ? ctx->shape : (var == 17 ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;

@@ -67,13 +67,14 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 
 }  // namespace copy2
 
-template <int G, int U, bool IMPLICIT>
+template <int G, int U, bool IMPLICIT, int UW0 = 0>
 __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
     constexpr int GPB = 256 / G;
-    // generic slots loaded before the parse: the window plus at least 8 chunks past it
-    constexpr int UW = (WIN_CH + 8 + G - 1) / G;
-    constexpr uint32_t NEX = (uint32_t)(UW * G - WIN_CH);  // generic chunks past the window in that round
+    // slots per lane loaded before the parse (UW0, or enough for the window plus 8 chunks past it):
+    // the window, then the generic chunks past it, then the first body chunks
+    constexpr int UW = UW0 > 0 ? UW0 : (WIN_CH + 8 + G - 1) / G;
+    constexpr uint32_t NEX = (uint32_t)(UW * G - WIN_CH);  // chunks past the window in that round
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     __shared__ u32x4 win[GPB][WIN_CH];
     __shared__ Geom geo[GPB];
@@ -109,6 +110,11 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         const uint32_t n2 = nch > kb1 ? nch - kb1 : 0u;
         const uint32_t ne = n1 + n2;
         auto gen_k = [&](uint32_t e) -> uint32_t { return e < n1 ? WIN_CH + e : kb1 + (e - n1); };
+        const uint32_t nb = kb1 - kb0;
+        // body chunks that ride in round 1's spare slots (built there the generic way)
+        const uint32_t body1 = ne < NEX ? (nb < NEX - ne ? nb : NEX - ne) : 0u;
+        // chunk of round-1 slot e past the window: generic chunks, then body chunks
+        auto ext_k = [&](uint32_t e) -> uint32_t { return e < ne ? gen_k(e) : kb0 + (e - ne); };
 
         // a generic chunk: the destination chunk (unless it is all payload) and the two aligned
         // source chunks under its payload bytes (clamped into the source range's aligned chunks:
@@ -142,7 +148,6 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         };
 
         // body chunks: U per lane per round; their loads need only the copy range, not the parse
-        const uint32_t nb = kb1 - kb0;
         const uint64_t skA = sk & ~3ull;
         const uint32_t b = (uint32_t)(sk & 3u);
         auto body_load = [&](uint32_t i0, u32x4* lo, uint32_t* hi) {
@@ -168,15 +173,15 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             for (int u = 0; u < UW; ++u) {
                 const uint32_t j = (uint32_t)(u * G + lane);
                 const bool w = j < (uint32_t)WIN_CH;
-                const uint32_t k = w ? j : gen_k(j - WIN_CH);
-                const bool in = w ? j < nch : j - WIN_CH < ne;
+                const uint32_t k = w ? j : ext_k(j - WIN_CH);
+                const bool in = w ? j < nch : j - WIN_CH < ne + body1;
                 gen_load(k, in, d[u], c0[u], c1[u]);
             }
 #pragma unroll
             for (int u = 0; u < UW; ++u) {
                 const uint32_t j = (uint32_t)(u * G + lane);
                 const bool w = j < (uint32_t)WIN_CH;
-                const uint32_t k = w ? j : gen_k(j - WIN_CH);
+                const uint32_t k = w ? j : ext_k(j - WIN_CH);
                 gm[u] = gen_merge(k, d[u], c0[u], c1[u]);
                 if (w && j < nch) wn[j] = gm[u];
             }
@@ -219,8 +224,8 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         for (int u = 0; u < UW; ++u) {
             const uint32_t j = (uint32_t)(u * G + lane);
             const bool w = j < (uint32_t)WIN_CH;
-            const uint32_t k = w ? j : gen_k(j - WIN_CH);
-            const bool in = w ? j < nch : j - WIN_CH < ne;
+            const uint32_t k = w ? j : ext_k(j - WIN_CH);
+            const bool in = w ? j < nch : j - WIN_CH < ne + body1;
             if (in) {
                 const int pos = (int)(16u * k) - (int)head;
                 acc = sum_chunk(gm[u], pos, s1, acc);
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         }
 
         // ---- body: copy + sum ----
-        for (uint32_t i0 = 0; i0 < nb; i0 += (uint32_t)(G * U)) {
+        for (uint32_t i0 = body1; i0 < nb; i0 += (uint32_t)(G * U)) {
             body_load(i0, blo, bhi);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -276,30 +281,33 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     }
 }
 
-template <bool IMPLICIT, int G, int U>
+template <bool IMPLICIT, int G, int U, int UW = 0>
 hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT>), dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
-// Shapes (lanes per record x body chunks per lane per round).  16 x 3, the default, takes a C2copy
-// body (85 chunks) in two rounds: 0.7085-0.743 ms on MI355X against 0.761-0.842 for 8 x 6, 0.805 for
-// 16 x 4, 0.85 for 16 x 6 and 1.05-1.08 for 32 x 3 (tools/exp_copy.py).
+// Shapes (lanes per record x body chunks per lane per round [x round-1 slots per lane]).  The
+// default, 16 x 4 x 2, takes a C2copy record in two rounds: the window, its last chunk and 23 body
+// chunks, then the other 62 body chunks.  Measured on one MI355X (tools/exp_copy.py): 16 x 4 x 2
+// 0.738 ms, 16 x 3 0.760, 16 x 3 x 2 0.790, 8 x 4 x 4 0.790, 8 x 6 0.837, 32 x 2 1.03, 64 x 2 1.73
+// (variant 16: 0.772); per-record work (parse, gates, window stores) is issued once per wavefront
+// for its 64 / G records, so wide groups pay it for fewer records, narrow ones need more rounds.
 template <bool IMPLICIT>
 hipError_t launch_copy2(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (shape) {
         case CFG_G8U6: return launch_copy2_one<IMPLICIT, 8, 6>(p, max_blocks, s);
-        case CFG_G8U7: return launch_copy2_one<IMPLICIT, 8, 4>(p, max_blocks, s);
-        case CFG_G16U4: return launch_copy2_one<IMPLICIT, 16, 4>(p, max_blocks, s);
-        case CFG_G16U6: return launch_copy2_one<IMPLICIT, 16, 6>(p, max_blocks, s);
-        case CFG_G32U3: return launch_copy2_one<IMPLICIT, 32, 3>(p, max_blocks, s);
-        case CFG_G32U4: return launch_copy2_one<IMPLICIT, 32, 2>(p, max_blocks, s);
+        case CFG_G8U7: return launch_copy2_one<IMPLICIT, 8, 4, 4>(p, max_blocks, s);
+        case CFG_G16U4: return launch_copy2_one<IMPLICIT, 16, 4, 2>(p, max_blocks, s);
+        case CFG_G16U6: return launch_copy2_one<IMPLICIT, 16, 3, 2>(p, max_blocks, s);
+        case CFG_G32U3: return launch_copy2_one<IMPLICIT, 32, 2, 1>(p, max_blocks, s);
+        case CFG_G32U4: return launch_copy2_one<IMPLICIT, 32, 3, 1>(p, max_blocks, s);
         case CFG_G64U2:
         case CFG_G64U4: return launch_copy2_one<IMPLICIT, 64, 2>(p, max_blocks, s);
-        default: return launch_copy2_one<IMPLICIT, 16, 3>(p, max_blocks, s);
+        default: return launch_copy2_one<IMPLICIT, 16, 3>(p, max_blocks, s);  // CFG_G16U3
     }
 }
 
