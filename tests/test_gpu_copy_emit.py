@@ -301,3 +301,23 @@ def test_copy_emit_far_fields(eng, variant):
     for shape in (-1, 1, 3):
         st, got, _, _ = _run(eng, recs, spec, gap_seed=13, seed=14 + shape, variant=variant, shape=shape)
         assert (st & E.ST_MALFORMED).sum() == 0
+
+
+@pytest.mark.parametrize("variant", COPY_VARIANTS)
+def test_copy_emit_tiny_records(eng, variant):
+    """Records of 0 .. 47 bytes (shorter than the header window, than one 16-B chunk, or empty)
+    packed at odd offsets, with copy ranges anywhere inside them (or not fitting)."""
+    rng = np.random.default_rng(33)
+    recs, spec = [], []
+    for i in range(900):
+        n = int(rng.integers(0, 48))
+        if i % 3 == 0 and n >= 28:
+            r = P.ipv4(V4A, V4B, 17, P.udp(i, 9, P.rand_bytes(rng, n - 28)))
+        else:
+            r = P.rand_bytes(rng, n)
+        recs.append(r)
+        d0 = int(rng.integers(0, n + 1))
+        ln = int(rng.integers(0, n - d0 + 2))  # sometimes one byte too long: MALFORMED, untouched
+        spec.append((d0, ln))
+    for shape in (-1, 0, 1):
+        _run(eng, recs, spec, gap_seed=17, seed=18 + shape, variant=variant, shape=shape)
