@@ -38,7 +38,8 @@ int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum
  * 0: 8 x 6, 1: 16 x 3, 2: 16 x 6, 3: 32 x 3, 4: 32 x 4, 5: 64 x 2, 6: 64 x 4, 7: 8 x 7, 8: 16 x 4. */
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
-/* Kernel variant (-1 = automatic: 7 for emit over descriptor batches, 5 otherwise).  The
+/* Kernel variant (-1 = automatic: 7 for emit over descriptor batches, 13 for verify over
+ * descriptor batches, 5 otherwise; 17 for copy-emit).  The
  * "walk" kernel (a group parses and finishes its own record) reads 16-byte chunks on a grid that
  * starts at the record's 16-byte boundary: 0 = non-temporal loads + register prefetch of the next
  * step, 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch; or at its
@@ -46,9 +47,14 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
  * 3 / 4 = the "tile" kernel (groups only stream and sum, lanes finish 64 records at once) with
  * non-temporal / plain loads on the 16-byte grid, 7 = the tile kernel with non-temporal loads on
  * the line grid — emit and verify only (data() uses the walk kernel).  8 = the walk kernel on the
- * 16-byte grid with plain loads and no prefetch (copy-emit's default).  9 / 10 = variant 5 with the
- * first two / the first 16-byte chunk of every lane's step loaded cached, so that the lines holding
- * the fields are resident in L2 when emit stores them (fixed-stride emit only; elsewhere 5). */
+ * 16-byte grid with plain loads and no prefetch.  9 / 10 = variant 5 with the first two / the first
+ * 16-byte chunk of every lane's step loaded cached, so that the lines holding the fields are
+ * resident in L2 when emit stores them (fixed-stride emit only; elsewhere 5).  13 = variant 5
+ * without the prefetch.  Copy-emit: 1 / 8 / 11 / 16 = the walk kernel in its copy mode (prefetch /
+ * two aligned source chunks / one chunk + the next lane's / dword-aligned source + one dword from
+ * the next lane); 17 (default) = copy_kernel (csum_copy.hip), whose shapes are 16 x 4 with two
+ * round-1 slots per lane (default, shape 8), 16 x 3 (1), 8 x 6 (0), 8 x 4 (7), 16 x 6 (2), 32 x 3 (3),
+ * 32 x 2 (4), 64 x 2 (5, 6). */
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
 
 /* Tile kernel: records per wavefront tile, 32 (default) or 64. */

@@ -961,7 +961,8 @@ hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_bl
 
 // MODE_COPY keeps three chunks per lane and step (record + two source chunks), so it is built for
 // the U <= 3 shapes only (wider shapes map to the same group size with fewer chunks) and for the
-// plain-load variants on the 16-byte grid.  Without the register prefetch (variant 8, the default)
+// plain-load variants on the 16-byte grid.  (Copy-emit's default is now variant 17, copy_kernel in
+// csum_copy.hip.)  Without the register prefetch (variant 8, round 1's default)
 // the kernel needs fewer VGPRs and runs more waves per SIMD: C2 copy-emit 0.95 -> 0.85 ms on
 // MI355X (tools/gpu_exp.sh sweep, profiles/r01_kernel_stats_c2copy.csv); variant 1 keeps the
 // prefetch for comparison.
