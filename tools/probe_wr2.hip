@@ -9,6 +9,8 @@
 //   4 scatter only: the two 2-B stores per record, no reads (stride 1536)
 //   5 scatter only at stride 4608 (three times the buffer span per store)
 //   6 as 1, the first line loaded with a plain (cached) load
+//   7 as 1, stores as the whole first 64-B line (the line's bytes, patched)
+//   8 as 1, stores as the whole first 128-B line
 // Standalone tool; results in DESIGN.md §5.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -69,8 +71,8 @@ __global__ __launch_bounds__(256) void rw(uint8_t* buf, uint64_t n, uint32_t str
     acc = red16(acc);
     if (MODE == 0) {
         if (acc == 0x12345678u) buf[0] = 1;
-    } else if (MODE == 3) {
-        if (lane < 4) {
+    } else if (MODE == 3 || MODE == 7 || MODE == 8) {
+        if (lane < (MODE == 8 ? 8 : 4)) {
             u32x4 c = head;
             if (lane == 0) c.z = (c.z & 0xffff0000u) | (acc & 0xffffu);
             if (lane == 1) c.z = (c.z & 0xffff0000u) | (acc >> 16);
@@ -92,10 +94,11 @@ int main() {
     CK(hipEventCreate(&b));
     const char* names[] = {"read only", "loads at once + 2x2B stores", "first line last + 2x2B stores",
                            "first line last + 64-B line store", "scatter only, stride 1536", "scatter only, stride 4608",
-                           "first line cached + 2x2B stores"};
+                           "first line cached + 2x2B stores", "loads at once + 64-B line store",
+                           "loads at once + 128-B line store"};
     const dim3 g((unsigned)(n / 16)), blk(256);
     for (int rnd = 0; rnd < 3; ++rnd)
-        for (int m = 0; m < 7; ++m) {
+        for (int m = 0; m < 9; ++m) {
             auto run = [&]() {
                 switch (m) {
                     case 0: hipLaunchKernelGGL(rw<0>, g, blk, 0, 0, buf, n, 1536u); break;
@@ -104,7 +107,9 @@ int main() {
                     case 3: hipLaunchKernelGGL(rw<3>, g, blk, 0, 0, buf, n, 1536u); break;
                     case 4: hipLaunchKernelGGL(rw<4>, g, blk, 0, 0, buf, n, 1536u); break;
                     case 5: hipLaunchKernelGGL(rw<5>, g, blk, 0, 0, buf, n, 4608u); break;
-                    default: hipLaunchKernelGGL(rw<6>, g, blk, 0, 0, buf, n, 1536u); break;
+                    case 6: hipLaunchKernelGGL(rw<6>, g, blk, 0, 0, buf, n, 1536u); break;
+                    case 7: hipLaunchKernelGGL(rw<7>, g, blk, 0, 0, buf, n, 1536u); break;
+                    default: hipLaunchKernelGGL(rw<8>, g, blk, 0, 0, buf, n, 1536u); break;
                 }
             };
             for (int i = 0; i < 3; ++i) run();
