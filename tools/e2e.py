@@ -3,7 +3,7 @@
 
 The reference path starts and ends in host memory (the phy device buffer / loopback ring), so
 BASELINE.json asks for the rate including pinned hipMemcpyAsync both ways.  Pipeline per chunk,
-three HIP streams, double-buffered device chunks:
+three HIP streams, `--buffers` device chunks in rotation (default 2: double-buffered):
 
     TX:  H2D(frames) -> smol_csum_batch_emit -> D2H(frames with checksums)
     RX:  H2D(frames) -> smol_csum_batch_verify -> D2H(status bytes)
@@ -11,7 +11,7 @@ three HIP streams, double-buffered device chunks:
 Reported: record bytes per second through the whole pipeline, next to the bare PCIe copy rates
 measured in the same process.
 
-    python tools/e2e.py [--records N] [--chunk M]
+    python tools/e2e.py [--records N] [--chunk M] [--buffers B]
 """
 from __future__ import annotations
 
@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(n_records: int = 1 << 20, chunk: int = 1 << 17, L: int = 1500, reps: int = 3, device: int = 0):
+def run(n_records: int = 1 << 20, chunk: int = 1 << 17, L: int = 1500, reps: int = 3, device: int = 0, nbuf: int = 2):
     import torch
 
     from smoltcp_amd import engine as E
@@ -44,8 +44,8 @@ def run(n_records: int = 1 << 20, chunk: int = 1 << 17, L: int = 1500, reps: int
         eng.synth(tmp, b, E.SYNTH_UDP4, seed=0x5EED0001 + c)
         host_in[c * chunk * L:(c * chunk + m) * L].copy_(tmp[:m * L])
     torch.cuda.synchronize()
-    dbuf = [torch.empty(chunk * L, dtype=torch.uint8, device=dev) for _ in range(2)]
-    dst = [torch.empty(chunk, dtype=torch.uint8, device=dev) for _ in range(2)]
+    dbuf = [torch.empty(chunk * L, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    dst = [torch.empty(chunk, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     s_h2d, s_cmp, s_d2h = (torch.cuda.Stream(dev) for _ in range(3))
 
     def pipeline(mode: str):
@@ -54,11 +54,11 @@ def run(n_records: int = 1 << 20, chunk: int = 1 << 17, L: int = 1500, reps: int
         e_d2h = [torch.cuda.Event() for _ in range(nchunks)]
         for c in range(nchunks):
             m = min(chunk, n_records - c * chunk)
-            k = c % 2
+            k = c % nbuf
             lo, hi = c * chunk * L, (c * chunk + m) * L
             with torch.cuda.stream(s_h2d):
-                if c >= 2:
-                    s_h2d.wait_event(e_d2h[c - 2])  # the device chunk is free again
+                if c >= nbuf:
+                    s_h2d.wait_event(e_d2h[c - nbuf])  # the device chunk is free again
                 dbuf[k][:m * L].copy_(host_in[lo:hi], non_blocking=True)
                 e_h2d[c].record(s_h2d)
             with torch.cuda.stream(s_cmp):
@@ -86,22 +86,32 @@ def run(n_records: int = 1 << 20, chunk: int = 1 << 17, L: int = 1500, reps: int
         return (time.perf_counter() - t0) / reps
 
     total = n_records * L
-    res = {"records": n_records, "record_bytes": L, "chunk_records": chunk}
+    res = {"records": n_records, "record_bytes": L, "chunk_records": chunk, "device_buffers": nbuf}
     # bare copy rates over the same bytes
     def h2d():
         for c in range(nchunks):
             m = min(chunk, n_records - c * chunk)
-            dbuf[c % 2][:m * L].copy_(host_in[c * chunk * L:(c * chunk + m) * L], non_blocking=True)
+            dbuf[c % nbuf][:m * L].copy_(host_in[c * chunk * L:(c * chunk + m) * L], non_blocking=True)
         torch.cuda.synchronize()
 
     def d2h():
         for c in range(nchunks):
             m = min(chunk, n_records - c * chunk)
-            host_out[c * chunk * L:(c * chunk + m) * L].copy_(dbuf[c % 2][:m * L], non_blocking=True)
+            host_out[c * chunk * L:(c * chunk + m) * L].copy_(dbuf[c % nbuf][:m * L], non_blocking=True)
+        torch.cuda.synchronize()
+
+    def duplex():  # H2D and D2H of the same bytes at once, on two streams (what TX needs)
+        for c in range(nchunks):
+            m = min(chunk, n_records - c * chunk)
+            with torch.cuda.stream(s_h2d):
+                dbuf[c % nbuf][:m * L].copy_(host_in[c * chunk * L:(c * chunk + m) * L], non_blocking=True)
+            with torch.cuda.stream(s_d2h):
+                host_out[c * chunk * L:(c * chunk + m) * L].copy_(dbuf[(c + 1) % nbuf][:m * L], non_blocking=True)
         torch.cuda.synchronize()
 
     res["h2d_GBs"] = round(total / timed(h2d) / 1e9, 2)
     res["d2h_GBs"] = round(total / timed(d2h) / 1e9, 2)
+    res["duplex_each_way_GBs"] = round(total / timed(duplex) / 1e9, 2)
     t_tx = timed(lambda: pipeline("tx"))
     t_rx = timed(lambda: pipeline("rx"))
     res["tx_emit_e2e_GBs"] = round(total / t_tx / 1e9, 2)
@@ -128,8 +138,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=1 << 20)
     ap.add_argument("--chunk", type=int, default=1 << 17)
+    ap.add_argument("--buffers", type=int, default=2)
     args = ap.parse_args()
-    print(json.dumps(run(args.records, args.chunk)))
+    print(json.dumps(run(args.records, args.chunk, nbuf=args.buffers)))
 
 
 if __name__ == "__main__":
