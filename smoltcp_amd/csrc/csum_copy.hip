@@ -150,6 +150,10 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         // body chunks: U per lane per round; their loads need only the copy range, not the parse
         const uint64_t skA = sk & ~3ull;
         const uint32_t b = (uint32_t)(sk & 3u);
+        // the dword after a chunk's 16 source bytes holds its last b bytes; no lane of the wavefront
+        // needs it when every record it holds has b == 0 (source and destination co-aligned mod 4,
+        // as in C2copy), and then those loads are not issued at all
+        const bool need_hi = __any(b != 0u);
         auto body_load = [&](uint32_t i0, u32x4* lo, uint32_t* hi) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -157,9 +161,8 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
                 const bool in = i < nb;
                 const uint64_t A = skA + 16ull * (kb0 + i);
                 lo[u] = ld16<false>((gcv4)(in ? A : dummy));
-                // the dword after them holds the chunk's last b bytes (none when b == 0: that dword
-                // may lie past the source range)
-                hi[u] = *(const GMEM uint32_t*)(in && b ? A + 16 : dummy);
+                // (b == 0: that dword may lie past the source range, so it is not read)
+                hi[u] = need_hi ? *(const GMEM uint32_t*)(in && b ? A + 16 : dummy) : 0u;
             }
         };
         u32x4 blo[U];
