@@ -52,9 +52,9 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
  * resident in L2 when emit stores them (fixed-stride emit only; elsewhere 5).  13 = variant 5
  * without the prefetch.  Copy-emit: 1 / 8 / 11 / 16 = the walk kernel in its copy mode (prefetch /
  * two aligned source chunks / one chunk + the next lane's / dword-aligned source + one dword from
- * the next lane); 17 (default) = copy_kernel (csum_copy.hip), whose shapes are 16 x 4 with two
- * round-1 slots per lane (default, shape 8), 16 x 3 (1), 8 x 6 (0), 8 x 4 (7), 16 x 6 (2), 32 x 3 (3),
- * 32 x 2 (4), 64 x 2 (5, 6). */
+ * the next lane); 17 (default) = copy_kernel (csum_copy.hip), whose shapes are 16 x 4 with 32 body
+ * chunks in round 1 (default, shape 8), 16 x 3 (1), 8 x 6 (0), 8 x 4 (7), 16 x 5 (2), 16 x 4 with
+ * the body chunks of round 1 built the generic way (3), 32 x 2 (4), 64 x 2 (5, 6). */
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
 
 /* Tile kernel: records per wavefront tile, 32 (default) or 64. */

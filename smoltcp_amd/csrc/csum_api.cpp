@@ -161,9 +161,9 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const hipStream_t s = (hipStream_t)stream;
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
         // default: variant 17 (csum_copy.hip: body chunks = one source load + shift + sum + store,
-        // window and edge chunks generic) at 16 x 4 with two round-1 slots per lane: C2copy 0.772-0.853
-        // ms (variant 16) -> 0.709-0.760 ms (16 x 3) -> 0.738 ms (16 x 4, same box as 0.760)
-        // (tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 stay selectable.
+        // window and edge chunks generic) at its default shape (16 x 4, round 1 carrying 32 body
+        // chunks): C2copy 0.772-0.853 ms (variant 16) -> 0.689 ms (tools/exp_copy.py, MI355X).
+        // Variants 1 / 8 / 11 / 16 stay selectable.
         const int cv = ctx->variant;
         const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? cv : 17;
         const int cshape = ctx->shape >= 0 ? ctx->shape : (var == 17 ? (int)CFG_G16U4 : shape);

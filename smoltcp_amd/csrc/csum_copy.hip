@@ -9,15 +9,16 @@
 // A group of G lanes owns a record.  Its 16-B destination chunks fall into two classes:
 // * BODY chunks lie past the 128-B header window and entirely inside the copy range.  A lane reads
 //   the 16 source bytes from the chunk's first source byte rounded down to 4 (one dwordx4 load) and
-//   the dword after them (one dword load), shifts them to the destination alignment with four
-//   v_alignbyte, sums them and stores them: no destination load, no mask, no neighbour exchange.
-//   That loop is unrolled U deep, all loads issued first.
+//   the dword after them (one dword load, not issued when no record of the wavefront needs it),
+//   shifts them to the destination alignment with four v_alignbyte, sums them and stores them: no
+//   destination load, no mask, no neighbour exchange.  That loop is unrolled U deep, all loads
+//   issued first.
 // * GENERIC chunks — the window (the first 128 B of the chunk grid, which hold the headers the gates
 //   parse) and any chunk past it that holds bytes outside the copy range (normally just the
 //   record's last chunk) — are built from the destination chunk and two aligned source chunks with
-//   byte masks.  The window and the first few other generic chunks are loaded in ONE round before
-//   the parse, so a C2copy record takes one round trip for its headers and tail, then
-//   ceil(body / (G * U)) for its body.
+//   byte masks.  The window, the first few other generic chunks and the first UB * G body chunks are
+//   loaded in ONE round before the parse, so a C2copy record takes one round trip for its headers,
+//   tail and first body chunks, then one for the rest of its body.
 // Every byte of the record is written (bytes outside the copy range with their own values, so no
 // line is left half-written by this kernel); the window chunks go out last from LDS, with the
 // fields finish_gates patched in.  A field past the window (behind a long IPv6 Hop-by-Hop header)
@@ -67,7 +68,7 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 
 }  // namespace copy2
 
-template <int G, int U, bool IMPLICIT, int UW0 = 0>
+template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0>
 __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
     constexpr int GPB = 256 / G;
@@ -112,7 +113,9 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         auto gen_k = [&](uint32_t e) -> uint32_t { return e < n1 ? WIN_CH + e : kb1 + (e - n1); };
         const uint32_t nb = kb1 - kb0;
         // body chunks that ride in round 1's spare slots (built there the generic way)
-        const uint32_t body1 = ne < NEX ? (nb < NEX - ne ? nb : NEX - ne) : 0u;
+        // (UB > 0: none; the first UB * G body chunks are loaded the body way in round 1 instead)
+        const uint32_t body1 = UB == 0 && ne < NEX ? (nb < NEX - ne ? nb : NEX - ne) : 0u;
+        const uint32_t nbe = UB > 0 ? (nb < (uint32_t)(UB * G) ? nb : (uint32_t)(UB * G)) : 0u;
         // chunk of round-1 slot e past the window: generic chunks, then body chunks
         auto ext_k = [&](uint32_t e) -> uint32_t { return e < ne ? gen_k(e) : kb0 + (e - ne); };
 
@@ -154,6 +157,12 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         // needs it when every record it holds has b == 0 (source and destination co-aligned mod 4,
         // as in C2copy), and then those loads are not issued at all
         const bool need_hi = __any(b != 0u);
+        auto body_load1 = [&](uint32_t i, u32x4& lo, uint32_t& hi) {
+            const bool in = i < nb;
+            const uint64_t A = skA + 16ull * (kb0 + i);
+            lo = ld16<false>((gcv4)(in ? A : dummy));
+            hi = need_hi ? *(const GMEM uint32_t*)(in && b ? A + 16 : dummy) : 0u;
+        };
         auto body_load = [&](uint32_t i0, u32x4* lo, uint32_t* hi) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -167,6 +176,8 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         };
         u32x4 blo[U];
         uint32_t bhi[U];
+        u32x4 elo[UB > 0 ? UB : 1];
+        uint32_t ehi[UB > 0 ? UB : 1];
 
         // ---- round 1: the window and the first generic chunks past it ----
         u32x4 gm[UW];
@@ -179,6 +190,10 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
                 const uint32_t k = w ? j : ext_k(j - WIN_CH);
                 const bool in = w ? j < nch : j - WIN_CH < ne + body1;
                 gen_load(k, in, d[u], c0[u], c1[u]);
+            }
+            if constexpr (UB > 0) {
+#pragma unroll
+                for (int u = 0; u < UB; ++u) body_load1((uint32_t)(u * G + lane), elo[u], ehi[u]);
             }
 #pragma unroll
             for (int u = 0; u < UW; ++u) {
@@ -251,24 +266,32 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         }
 
         // ---- body: copy + sum ----
-        for (uint32_t i0 = body1; i0 < nb; i0 += (uint32_t)(G * U)) {
+        auto body_proc = [&](uint32_t i, const u32x4& lo, uint32_t hi) {
+            const uint32_t k = kb0 + i;
+            u32x4 m;
+            m.x = __builtin_amdgcn_alignbyte(lo.y, lo.x, b);
+            m.y = __builtin_amdgcn_alignbyte(lo.z, lo.y, b);
+            m.z = __builtin_amdgcn_alignbyte(lo.w, lo.z, b);
+            m.w = __builtin_amdgcn_alignbyte(hi, lo.w, b);
+            const int pos = (int)(16u * k) - (int)head;
+            acc = sum_chunk(m, pos, s1, acc);
+            const gu8 dst = (gu8)base + 16u * k;
+            if (!far) *(GMEM u32x4*)dst = m;
+            else store_part(dst, m, 0, 16, f0b - pos, f1b - pos, f2b - pos);
+        };
+        if constexpr (UB > 0) {
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                const uint32_t i = (uint32_t)(u * G + lane);
+                if (i < nbe) body_proc(i, elo[u], ehi[u]);
+            }
+        }
+        for (uint32_t i0 = UB > 0 ? nbe : body1; i0 < nb; i0 += (uint32_t)(G * U)) {
             body_load(i0, blo, bhi);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t i = i0 + (uint32_t)(u * G + lane);
-                if (i < nb) {
-                    const uint32_t k = kb0 + i;
-                    u32x4 m;
-                    m.x = __builtin_amdgcn_alignbyte(blo[u].y, blo[u].x, b);
-                    m.y = __builtin_amdgcn_alignbyte(blo[u].z, blo[u].y, b);
-                    m.z = __builtin_amdgcn_alignbyte(blo[u].w, blo[u].z, b);
-                    m.w = __builtin_amdgcn_alignbyte(bhi[u], blo[u].w, b);
-                    const int pos = (int)(16u * k) - (int)head;
-                    acc = sum_chunk(m, pos, s1, acc);
-                    const gu8 dst = (gu8)base + 16u * k;
-                    if (!far) *(GMEM u32x4*)dst = m;
-                    else store_part(dst, m, 0, 16, f0b - pos, f1b - pos, f2b - pos);
-                }
+                if (i < nb) body_proc(i, blo[u], bhi[u]);
             }
         }
 
@@ -284,33 +307,36 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     }
 }
 
-template <bool IMPLICIT, int G, int U, int UW = 0>
+template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0>
 hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW>), dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
-// Shapes (lanes per record x body chunks per lane per round [x round-1 slots per lane]).  The
-// default, 16 x 4 x 2, takes a C2copy record in two rounds: the window, its last chunk and 23 body
-// chunks, then the other 62 body chunks.  Measured on one MI355X (tools/exp_copy.py): 16 x 4 x 2
-// 0.738 ms, 16 x 3 0.760, 16 x 3 x 2 0.790, 8 x 4 x 4 0.790, 8 x 6 0.837, 32 x 2 1.03, 64 x 2 1.73
-// (variant 16: 0.772); per-record work (parse, gates, window stores) is issued once per wavefront
-// for its 64 / G records, so wide groups pay it for fewer records, narrow ones need more rounds.
+// Shapes (lanes per record x body chunks per lane per round [x generic round-1 slots per lane
+// [x body round-1 slots per lane]]).  The default, 16 x 4 x 1 x 2, takes a C2copy record in two
+// rounds: the window, its last chunk and 32 body chunks (loaded the body way), then the other 53.
+// Measured on one MI355X (tools/exp_copy.py, profiles/r02b_experiments/): 16 x 4 x 1 x 2 0.689 ms,
+// 16 x 5 x 1 x 1 0.691, 16 x 4 x 2 (body chunks in generic slots) 0.710, 16 x 3 0.743; earlier, before
+// the hi-dword loads were skipped: 16 x 4 x 2 0.738, 16 x 3 0.760, 8 x 4 x 4 0.790, 8 x 6 0.837,
+// 32 x 2 1.03, 64 x 2 1.73 (variant 16: 0.772).  Per-record work (parse, gates, window stores) is
+// issued once per wavefront for its 64 / G records, so wide groups pay it for fewer records,
+// narrow ones need more rounds.
 template <bool IMPLICIT>
 hipError_t launch_copy2(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (shape) {
         case CFG_G8U6: return launch_copy2_one<IMPLICIT, 8, 6>(p, max_blocks, s);
         case CFG_G8U7: return launch_copy2_one<IMPLICIT, 8, 4, 4>(p, max_blocks, s);
-        case CFG_G16U4: return launch_copy2_one<IMPLICIT, 16, 4, 2>(p, max_blocks, s);
-        case CFG_G16U6: return launch_copy2_one<IMPLICIT, 16, 3, 2>(p, max_blocks, s);
-        case CFG_G32U3: return launch_copy2_one<IMPLICIT, 32, 2, 1>(p, max_blocks, s);
-        case CFG_G32U4: return launch_copy2_one<IMPLICIT, 32, 3, 1>(p, max_blocks, s);
+        case CFG_G16U3: return launch_copy2_one<IMPLICIT, 16, 3>(p, max_blocks, s);
+        case CFG_G16U6: return launch_copy2_one<IMPLICIT, 16, 5, 1, 1>(p, max_blocks, s);
+        case CFG_G32U3: return launch_copy2_one<IMPLICIT, 16, 4, 2>(p, max_blocks, s);
+        case CFG_G32U4: return launch_copy2_one<IMPLICIT, 32, 2, 1>(p, max_blocks, s);
         case CFG_G64U2:
         case CFG_G64U4: return launch_copy2_one<IMPLICIT, 64, 2>(p, max_blocks, s);
-        default: return launch_copy2_one<IMPLICIT, 16, 3>(p, max_blocks, s);  // CFG_G16U3
+        default: return launch_copy2_one<IMPLICIT, 16, 4, 1, 2>(p, max_blocks, s);  // CFG_G16U4
     }
 }
 

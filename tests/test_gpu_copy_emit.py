@@ -187,7 +187,7 @@ COPY_VARIANTS = [-1, 1, 8, 11, 16, 17]
 
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
-@pytest.mark.parametrize("shape", [-1, 0, 1, 3, 5, 7])
+@pytest.mark.parametrize("shape", [-1, 0, 1, 2, 3, 4, 5, 7])
 def test_copy_emit_mixed_packed(eng, shape, variant):
     rng = np.random.default_rng(10 + shape)
     recs, spec = [], []
