@@ -51,6 +51,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "c2copy"])
     ap.add_argument("--n", type=int, default=0, help="records per GPU (default: the config's)")
+    ap.add_argument("--ramp-ms", type=float, default=300.0,
+                    help="untimed steps for at least this long before the W warm-up steps, so that the "
+                         "GPU's clocks have ramped up (0: none; profiles/r03_steps/)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
     ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
@@ -413,6 +416,17 @@ def main(argv=None):
         if ev is not None:
             ev[2].record(stream)
 
+    # Clock ramp: a freshly idle MI355X takes ~15 ms of sustained load before its kernels run at
+    # their steady-state speed (profiles/r03_steps/step_trace_c2_w5.json: verify 273 -> 245 us
+    # over the 20 timed steps after 5 warm-up steps; 234 us after 100).  Untimed steps for
+    # --ramp-ms of wall time come first, then the W warm-up steps the contract names.
+    ramp_steps, r0 = 0, time.perf_counter()
+    while (time.perf_counter() - r0) * 1e3 < args.ramp_ms:
+        for _ in range(8):
+            step()
+        ramp_steps += 8
+        torch.cuda.synchronize()
+    ramp_ms = (time.perf_counter() - r0) * 1e3
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -531,6 +545,9 @@ def main(argv=None):
                                  for k, v in kernels.items()},
             "kernel_timing": "HIP events at the kernel boundaries on the launch stream, over a second pass of "
                              "K steps after the timed region (the timed region has no events between kernels)",
+            "ramp": {"steps": ramp_steps, "ms": round(ramp_ms, 1),
+                     "what": "untimed steps before the W warm-up steps until the GPU clocks have ramped "
+                             "(steady state: profiles/r03_steps/)"},
             "verify_rejected": rejected,
             "per_rank": per_rank,
             "cpu_baseline": cpu,

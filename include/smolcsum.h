@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SMOLCSUM_ABI_VERSION 3
+#define SMOLCSUM_ABI_VERSION 4
 
 /* ---- error codes ------------------------------------------------------------------------ */
 enum {
@@ -97,9 +97,23 @@ typedef struct {
     uint64_t offset; /* byte offset of the record from the batch base pointer (any alignment) */
     uint32_t len;    /* record length in bytes, <= SMOL_MAX_RECORD_LEN                         */
     uint8_t kind;    /* SMOL_KIND_*                                                            */
-    uint8_t flags;   /* reserved, must be 0                                                    */
+    uint8_t flags;   /* SMOL_REC_* (0 for an ordinary record); other bits must be 0            */
     uint16_t reserved;
 } smol_csum_desc_t;
+
+/* Record flags (smol_csum_desc_t.flags, or smol_csum_batch_t.flags for every record of a
+ * fixed-stride batch).
+ *
+ * SMOL_REC_IPHDR_ONLY — a raw-socket frame.  A raw socket's L4 bytes go out as the user wrote
+ * them: dispatch copies IpPayload::Raw verbatim (src/iface/packet.rs:132-136) and only the IPv4
+ * header is emitted by the stack (Ipv4Repr::emit under caps.ipv4, src/socket/raw.rs:406-423).  On
+ * receive the raw socket sees the packet after the IPv4 header gate and before any L4 gate
+ * (src/iface/interface/ipv4.rs:150-151).  So for such a record emit fills (or zeroes) the IPv4
+ * header checksum only and never touches a byte past the IP header; verify applies the IPv4
+ * header gate only.  The record is reported SMOL_ST_UNSUPPORTED (no L4 checksum on its path), or
+ * SMOL_ST_MALFORMED when its IP header fails check_len.  In a fragment group the flag on any of
+ * the group's records makes the whole datagram raw. */
+#define SMOL_REC_IPHDR_ONLY 0x01u
 
 /* Batch geometry (host memory).  If `desc` is non-NULL it is a DEVICE array of `n` descriptors
  * and `stride`/`len`/`kind` are ignored.  Otherwise record i starts at base + i*stride, has
@@ -110,7 +124,8 @@ typedef struct {
     uint64_t stride;
     uint32_t len;
     uint8_t kind;
-    uint8_t reserved[3];
+    uint8_t flags;       /* SMOL_REC_* for every record of a fixed-stride batch (ignored with desc) */
+    uint8_t reserved[2]; /* must be 0 */
 } smol_csum_batch_t;
 
 /* ---- per-record status byte (verify; emit reports the MALFORMED/UNSUPPORTED bits) ------- */
@@ -124,8 +139,12 @@ enum {
     SMOL_ST_IP_VALID = 0x08,   /* Ipv4Packet::verify_checksum() regardless of caps (1 if no
                                   IPv4 header)                                                   */
     SMOL_ST_L4_VALID = 0x10,   /* the L4 verify_checksum() regardless of caps (1 if no L4 span)  */
-    SMOL_ST_MALFORMED = 0x20,  /* a check_len() on the path failed: the reference drops the
-                                  packet before any checksum is looked at                        */
+    SMOL_ST_MALFORMED = 0x20,  /* the reference's parse drops the packet before any checksum is
+                                  looked at: a check_len() on the path failed, or (verify only) a
+                                  port Repr::parse rejects first — UDP destination port 0
+                                  (udp.rs:246-248), TCP source or destination port 0
+                                  (tcp.rs:910-915).  The L4 bits are then not evaluated (set).
+                                  Emit never rejects ports: Repr::emit does not check them.      */
     SMOL_ST_UNSUPPORTED = 0x40,/* no L4 checksum on this record's path: IPv4 fragment, protocol
                                   smoltcp does not checksum, IPv6 next header other than a
                                   leading Hop-by-Hop + TCP/UDP/ICMPv6, non-IP ethertype          */
@@ -211,7 +230,9 @@ int smol_csum_batch_copy_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_c
 
 /* One IPv4 datagram carried by `count` consecutive records of a batch, starting at record
  * `first` (16 bytes, device memory): its fragments, in any order.  A group of one unfragmented
- * packet is allowed.  Groups must not share records. */
+ * packet is allowed.  Groups must not share records.  A group that does not lie inside the batch
+ * (first >= n, or count > n - first), whose count is 0 or above SMOL_MAX_FRAGMENTS, or whose
+ * reserved word is not 0 is invalid: none of its records is read or written, status included. */
 typedef struct {
     uint64_t first;
     uint32_t count;    /* 1 .. SMOL_MAX_FRAGMENTS */
@@ -225,17 +246,34 @@ typedef struct {
 /* Emit for IPv4 datagrams the stack fragmented under offloaded checksums.  The iface emits the
  * whole datagram with the device's caps (the L4 checksum written 0) and only then cuts it into
  * fragments that reach TxToken::consume one by one (src/iface/interface/mod.rs:1276-1331,
- * src/iface/interface/ipv4.rs:440-490), so the device, holding a datagram's fragments until the
+ * src/iface/interface/ipv4.rs:421-490), so the device, holding a datagram's fragments until the
  * last one, fills per group: every fragment's IPv4 header checksum (caps.ipv4, as
- * dispatch_ipv4_frag does) and the datagram's L4 checksum — computed over the reassembled payload
- * exactly as Repr::emit does on the whole datagram, ICMPv4 error messages' embedded header
- * included — written into the fragment that holds the field.  The result is bit-identical to
- * "emit the whole datagram, then fragment it".  A group is usable when every record is an IPv4
- * packet (Medium::Ip, or Ethernet with ethertype 0x0800) passing Ipv4Packet::check_len, all share
- * the reassembly key (ident, source, destination, protocol: ipv4.rs get_key), the payloads cover
- * [0, T) exactly once with exactly one last fragment (MF clear) ending at T; otherwise its records
- * are reported SMOL_ST_MALFORMED and only their own headers are filled.  `d_status` (nullable)
- * receives SMOL_ST_MALFORMED / SMOL_ST_UNSUPPORTED per record of every group. */
+ * dispatch_ipv4_frag does) and the datagram's L4 checksum over the reassembled datagram — its
+ * L4 length, its pseudo-header, ICMPv4 error messages' embedded header included — written into
+ * the fragment that holds the field.  That is the RFC 1071 / 768 / 793 checksum a receiver
+ * verifies, and the one smoltcp's own reassembling receive path accepts.
+ *
+ * Deliberate divergence from the reference's software route.  With its default caps the reference
+ * emits a datagram it will fragment into the whole fixed-size frag.buffer
+ * (FRAGMENTATION_BUFFER_SIZE bytes, mod.rs:1320; emit_payload gets &mut buffer[hl..],
+ * mod.rs:1263-1267, packet.rs:80-83,166-171):
+ *   - UDP: identical.  UdpPacket::fill_checksum covers the UDP length field's span (udp.rs:194-208).
+ *   - TCP: differs whenever the datagram is shorter than the buffer.  TcpPacket::fill_checksum
+ *     sums the whole buffer tail and puts its length in the pseudo-header (tcp.rs:616-626), so the
+ *     reference's fragments carry a checksum its own reassembling receiver rejects.
+ *   - ICMPv4 echo: identical only when the buffer tail past the datagram is zero;
+ *     Icmpv4Packet::fill_checksum sums the whole tail, stale bytes of earlier datagrams included
+ *     (icmpv4.rs:339-346, 502-503).  ICMPv4 error messages: the reference's emit panics on a tail
+ *     (copy_from_slice of unequal lengths, icmpv4.rs:529-530, 543-544).
+ * tests/test_frag_cpu.py restates that route (oracle_emit_like_dispatch_ip) and pins each case.
+ *
+ * A group is usable when every record is an IPv4 packet (Medium::Ip, or Ethernet with ethertype
+ * 0x0800) passing Ipv4Packet::check_len, all share the reassembly key (ident, source, destination,
+ * protocol: ipv4.rs get_key), the payloads cover [0, T) exactly once with exactly one last
+ * fragment (MF clear) ending at T; otherwise its records are reported SMOL_ST_MALFORMED and only
+ * their own headers are filled.  A group with SMOL_REC_IPHDR_ONLY on any record gets its headers
+ * only (a raw socket's datagram).  `d_status` (nullable) receives SMOL_ST_MALFORMED /
+ * SMOL_ST_UNSUPPORTED per record of every valid group. */
 int smol_csum_batch_emit_frag(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                               const smol_csum_frag_group_t* d_groups, uint64_t n_groups,
                               const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);

@@ -125,13 +125,13 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.oracle_batch_data.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, u8p]
     L.oracle_batch_data.restype = None
     L.oracle_batch_emit.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
-                                    ctypes.c_uint8, ctypes.POINTER(CapsC), u8p]
+                                    ctypes.c_uint32, ctypes.POINTER(CapsC), u8p]
     L.oracle_batch_emit.restype = None
     L.oracle_batch_verify.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
-                                      ctypes.c_uint8, ctypes.POINTER(CapsC), u8p]
+                                      ctypes.c_uint32, ctypes.POINTER(CapsC), u8p]
     L.oracle_batch_verify.restype = None
     L.oracle_batch_copy_emit.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
-                                         ctypes.c_uint8, ctypes.POINTER(CapsC), u8p, u8p, u8p]
+                                         ctypes.c_uint32, ctypes.POINTER(CapsC), u8p, u8p, u8p]
     L.oracle_batch_copy_emit.restype = None
     L.oracle_nhc_udp_verify.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.POINTER(CapsC)]
     L.oracle_nhc_udp_verify.restype = ctypes.c_uint8
@@ -139,7 +139,7 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.oracle_nhc_udp_emit.restype = ctypes.c_uint8
     for name in ("oracle_batch_emit_frag", "oracle_batch_verify_frag"):
         f = getattr(L, name)
-        f.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint8, u8p,
+        f.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u8p,
                       ctypes.c_uint64, ctypes.POINTER(CapsC), u8p]
         f.restype = None
     for name in ("oracle_batch_nhc_udp_emit", "oracle_batch_nhc_udp_verify"):
@@ -147,7 +147,26 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
         f.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, u8p,
                       ctypes.POINTER(CapsC), u8p]
         f.restype = None
+    L.oracle_emit_like_dispatch_ip.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(CapsC)]
+    L.oracle_emit_like_dispatch_ip.restype = ctypes.c_int
     return L
+
+
+# SMOL_REC_IPHDR_ONLY (include/smolcsum.h): a raw-socket record; the oracle's batch functions take
+# a record's flags in bits 8..15 of `kind` (descriptor batches: smol_csum_desc_t.flags).
+REC_IPHDR_ONLY = 0x01
+
+
+def kind_flags(kind: int, flags: int = 0) -> int:
+    return int(kind) | (int(flags) << 8)
+
+
+def emit_like_dispatch_ip(frag_buffer: np.ndarray, caps=(0, 0, 0, 0, 0)) -> int:
+    """The reference's own route for a datagram it fragments (csum_oracle.c): the L4 checksum filled
+    over frag.buffer[hl..] (the datagram's L4 bytes + the stale tail), in place.  Returns 0, -1
+    (dropped / not IPv4) or -2 (the reference panics)."""
+    c = caps_c(caps)
+    return int(lib().oracle_emit_like_dispatch_ip(_ptr(frag_buffer), frag_buffer.size, ctypes.byref(c)))
 
 
 def _ptr(a: np.ndarray) -> int:

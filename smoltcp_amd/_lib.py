@@ -68,7 +68,8 @@ class BatchC(ctypes.Structure):
         ("stride", ctypes.c_uint64),
         ("len", ctypes.c_uint32),
         ("kind", ctypes.c_uint8),
-        ("reserved", ctypes.c_uint8 * 3),
+        ("flags", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 2),
     ]
 
 

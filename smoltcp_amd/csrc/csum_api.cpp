@@ -111,6 +111,7 @@ int check_batch(const smol_csum_batch_t* b, const void* d_buf) {
     if (!b) return SMOL_EINVAL;
     if (b->n == 0) return SMOL_OK;
     if (!d_buf) return SMOL_EINVAL;
+    if ((b->flags & ~SMOL_REC_IPHDR_ONLY) != 0 || b->reserved[0] != 0 || b->reserved[1] != 0) return SMOL_EINVAL;
     if (b->desc) {
         if (((uintptr_t)b->desc & 15u) != 0) return SMOL_EINVAL;
     } else if (b->len > SMOL_MAX_RECORD_LEN) {
@@ -132,7 +133,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.n = b->n;
     p.stride = b->stride;
     p.len = b->len;
-    p.kind = d_addrs ? KIND_NHC_UDP : b->kind;
+    p.kind = d_addrs ? KIND_NHC_UDP : (b->kind | ((b->flags & SMOL_REC_IPHDR_ONLY) ? KIND_IPHDR_ONLY : 0u));
     p.addrs = d_addrs;
     if (caps) {
         p.caps_ipv4 = caps->ipv4;
@@ -294,7 +295,7 @@ static int run_frag(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_c
     p.n = b->n;
     p.stride = b->stride;
     p.len = b->len;
-    p.kind = b->kind;
+    p.kind = b->kind | ((b->flags & SMOL_REC_IPHDR_ONLY) ? KIND_IPHDR_ONLY : 0u);
     p.caps_ipv4 = caps->ipv4;
     p.caps_udp = caps->udp;
     p.caps_tcp = caps->tcp;

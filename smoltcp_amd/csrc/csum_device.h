@@ -101,7 +101,8 @@ __host__ __device__ __forceinline__ uint32_t icmpv6_min_len(uint32_t t) {
 //   IPv6      Ipv6Packet::check_len src/wire/ipv6.rs:400-407, one leading Hop-by-Hop header
 //             src/iface/interface/ipv6.rs:205-211,300-303 (Ipv6ExtHeader::check_len,
 //             src/wire/ipv6ext_header.rs:55-69), next header dispatch :323-366
-//   L4        UdpPacket::check_len udp.rs:57-69, TcpPacket::check_len tcp.rs:155-167,
+//   L4        UdpPacket::check_len udp.rs:57-69, TcpPacket::check_len tcp.rs:155-167 (verify: and the
+//             port tests of UdpRepr::parse udp.rs:246-248 / TcpRepr::parse tcp.rs:910-915),
 //             Icmpv4Packet::check_len icmpv4.rs:207-214, IgmpPacket::check_len igmp.rs:73-80,
 //             Icmpv6Packet::check_len icmpv6.rs:274-338 (verify: the message-type lengths of
 //             icmpv6_min_len; emit: the generic len >= 4 — Icmpv6Packet::fill_checksum fills any type).
@@ -117,6 +118,10 @@ template <bool NHC = false, class RD>
 __device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint32_t kind, bool emit = false) {
     Geom g = {};
     uint32_t ip_off = 0;
+    // SMOL_REC_IPHDR_ONLY: a raw socket's frame, the IP header's gate only (src/socket/raw.rs:406-423,
+    // src/iface/packet.rs:132-136 on TX; src/iface/interface/ipv4.rs:150-151 on RX)
+    const bool hdr_only = (kind & KIND_IPHDR_ONLY) != 0;
+    kind &= 0xffu;
     if (NHC && kind == KIND_NHC_UDP) {
         if (len < 1) { g.st = SMOL_ST_MALFORMED; return g; }
         const uint32_t b0 = rd(0);
@@ -160,6 +165,7 @@ __device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint3
         g.ip_hl = hl;
         g.addr_off = ip_off + 12;
         g.addr_words = 4;
+        if (hdr_only) { g.st = SMOL_ST_UNSUPPORTED; return g; }
         const uint32_t b6 = rd(ip_off + 6);
         const uint32_t frag = ((b6 & 0x1fu) << 8) | rd(ip_off + 7);
         if ((b6 & 0x20u) || frag) { g.st = SMOL_ST_UNSUPPORTED; return g; }
@@ -179,6 +185,7 @@ __device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint3
         g.ip_off = ip_off;
         g.addr_off = ip_off + 8;
         g.addr_words = 16;
+        if (hdr_only) { g.st = SMOL_ST_UNSUPPORTED; return g; }
         uint32_t cur = ip_off + 40, rem = plen;
         uint32_t nh = rd(ip_off + 6);
         if (nh == 0) {  // Hop-by-Hop
@@ -205,6 +212,8 @@ __device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint3
             const uint32_t ul = (rd(l4 + 4) << 8) | rd(l4 + 5);
             if (g.l4_len < ul || ul < 8) { g.st = SMOL_ST_MALFORMED; break; }
             g.span_end = l4 + ul;
+            // UdpRepr::parse rejects destination port 0 before its checksum gate (udp.rs:246-248)
+            if (!emit && (rd(l4 + 2) | rd(l4 + 3)) == 0) g.st = SMOL_ST_MALFORMED;
             break;
         }
         case P_TCP: {
@@ -213,6 +222,8 @@ __device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint3
             const uint32_t thl = (rd(l4 + 12) >> 4) * 4;
             if (g.l4_len < thl || thl < 20) { g.st = SMOL_ST_MALFORMED; break; }
             g.span_end = l4 + g.l4_len;
+            // TcpRepr::parse rejects source or destination port 0 first (tcp.rs:910-915)
+            if (!emit && ((rd(l4) | rd(l4 + 1)) == 0 || (rd(l4 + 2) | rd(l4 + 3)) == 0)) g.st = SMOL_ST_MALFORMED;
             break;
         }
         case P_ICMP4:

@@ -82,9 +82,12 @@ __global__ __launch_bounds__(64) void frag_kernel(KParams p, const smol_csum_fra
     for (uint64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
         const uint64_t first = groups[gi].first;
         const uint32_t count = groups[gi].count;
-        if (count == 0 || count > MAXF) continue;
+        // an invalid group (outside the batch, count 0 or > SMOL_MAX_FRAGMENTS, reserved != 0) is
+        // not read or written at all (include/smolcsum.h)
+        if (first >= p.n || count == 0 || count > MAXF || count > p.n - first || groups[gi].reserved != 0) continue;
 
         // ---- 1. the fragments' IPv4 headers ----
+        // record j of the group: address, length, SMOL_KIND_* (+ KIND_IPHDR_ONLY for a raw frame)
         auto rec = [&](uint32_t j, uint64_t& a0, uint32_t& len, uint32_t& kind) {
             const uint64_t r = first + j;
             if (IMPLICIT) {
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(64) void frag_kernel(KParams p, const smol_csum_fra
                 const u32x4 d = *(gcv4)((uint64_t)p.desc + 16 * r);
                 a0 = (uint64_t)p.buf + ((uint64_t)d.x | ((uint64_t)d.y << 32));
                 len = d.z;
-                kind = d.w & 0xffu;
+                kind = desc_kind(d.w);
             }
         };
         // fragment 0's reassembly key (ipv4.rs get_key: ident, src, dst, protocol) and addresses
@@ -105,18 +108,21 @@ __global__ __launch_bounds__(64) void frag_kernel(KParams p, const smol_csum_fra
             uint64_t a0;
             uint32_t len, kind;
             rec(0, a0, len, kind);
+            kind &= 0xffu;
             const uint32_t io = kind == SMOL_KIND_ETH ? 14u : 0u;
             if ((kind == SMOL_KIND_IP || kind == SMOL_KIND_ETH) && len >= io + 20) {
                 k0a = a0 + io;
                 k0ok = true;
             }
         }
-        bool bad = !k0ok;
+        bool bad = !k0ok, raw = false;
         uint32_t T = 0, sumlen = 0, lastn = 0;
         for (uint32_t j = (uint32_t)lane; j < count; j += 64) {
             uint64_t a0;
             uint32_t len, kind;
             rec(j, a0, len, kind);
+            raw = raw || (kind & KIND_IPHDR_ONLY) != 0;  // a raw socket's datagram: headers only
+            kind &= 0xffu;
             uint32_t io = 0, ok = 0, hl = 0, total = 0, start = 0, end = 0, mf = 0;
             if (kind == SMOL_KIND_ETH) {
                 io = 14;
@@ -171,6 +177,7 @@ __global__ __launch_bounds__(64) void frag_kernel(KParams p, const smol_csum_fra
         sumlen = wave_sum(sumlen);
         lastn = wave_sum(lastn);
         bad = wave_any(bad);
+        raw = wave_any(raw);
 
         // ---- 2. the group contract ----
         bool broken = bad || lastn != 1 || sumlen != T;
@@ -197,17 +204,21 @@ __global__ __launch_bounds__(64) void frag_kernel(KParams p, const smol_csum_fra
         uint32_t proto = P_NONE, st = 0, span_end = 0, fo = 0, in_hl = 0;
         if (broken) {
             st = SMOL_ST_MALFORMED;
+        } else if (raw) {
+            st = SMOL_ST_UNSUPPORTED;
         } else {
             const uint32_t pr = rb(k0a + 9);
             if (pr == P_UDP) {
                 fo = 6;
                 const uint32_t ul = T >= 8 ? (dg(4) << 8 | dg(5)) : 0u;
                 if (T < 8 || T < ul || ul < 8) st = SMOL_ST_MALFORMED;
+                else if (!EMIT && (dg(2) | dg(3)) == 0) st = SMOL_ST_MALFORMED;  // udp.rs:246-248
                 span_end = ul;
             } else if (pr == P_TCP) {
                 fo = 16;
                 const uint32_t thl = T >= 20 ? (dg(12) >> 4) * 4 : 0u;
                 if (T < 20 || T < thl || thl < 20) st = SMOL_ST_MALFORMED;
+                else if (!EMIT && ((dg(0) | dg(1)) == 0 || (dg(2) | dg(3)) == 0)) st = SMOL_ST_MALFORMED;  // tcp.rs:910-915
                 span_end = T;
             } else if (pr == P_ICMP4 || pr == P_IGMP) {
                 fo = 2;

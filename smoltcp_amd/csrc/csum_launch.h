@@ -13,6 +13,12 @@ enum { MODE_DATA = 0, MODE_EMIT = 1, MODE_VERIFY = 2, MODE_COPY = 3 };  // COPY:
 
 // Internal record kind of the 6LoWPAN NHC UDP entry points (never in a descriptor).
 constexpr uint32_t KIND_NHC_UDP = 0x10;
+// Internal kind bit: SMOL_REC_IPHDR_ONLY (a raw socket's frame: the IP header's gate only).
+constexpr uint32_t KIND_IPHDR_ONLY = 0x200;
+// The kernels' view of a descriptor's kind byte + flags byte (the desc dword at offset 12).
+__host__ __device__ __forceinline__ uint32_t desc_kind(uint32_t w) {
+    return (w & 0xffu) | (((w >> 8) & SMOL_REC_IPHDR_ONLY) ? KIND_IPHDR_ONLY : 0u);
+}
 
 // Launch shapes: lanes per record (G) x 16-byte chunks per lane per step (U).
 enum {

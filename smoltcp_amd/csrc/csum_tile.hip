@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
             if ((uint32_t)lane < cnt) {
                 my_a0 = (uint64_t)p.buf + ((uint64_t)d.x | ((uint64_t)d.y << 32));
                 my_len = d.z;
-                my_kind = d.w & 0xffu;
+                my_kind = desc_kind(d.w);
             }
         }
 

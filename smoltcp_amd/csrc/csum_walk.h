@@ -111,7 +111,7 @@ __device__ __forceinline__ RecRef rec_at(const KParams& p, uint64_t r) {
         const u32x4 d = *(gcv4)((uint64_t)p.desc + 16 * r);
         rr.a0 = (uint64_t)p.buf + ((uint64_t)d.x | ((uint64_t)d.y << 32));
         rr.len = d.z;
-        rr.kind = NHC ? KIND_NHC_UDP : (d.w & 0xffu);  // NHC UDP entry points: every record
+        rr.kind = NHC ? KIND_NHC_UDP : desc_kind(d.w);  // NHC UDP entry points: every record
     }
     rr.sb = 0;
     rr.p0 = rr.p1 = 0;

@@ -20,6 +20,7 @@ from ._lib import BatchC, Caps, check, lib
 from .phy import ChecksumCapabilities
 
 KIND_RAW, KIND_IP, KIND_ETH = 0, 1, 2
+REC_IPHDR_ONLY = 0x01  # SMOL_REC_IPHDR_ONLY: a raw socket's frame (the IP header's gate only)
 
 ST_IP_OK = 0x01
 ST_L4_OK = 0x02
@@ -65,13 +66,14 @@ def make_copies(src_offsets, dst_offsets, lengths) -> np.ndarray:
     return c
 
 
-def make_descriptors(offsets, lengths, kinds) -> np.ndarray:
+def make_descriptors(offsets, lengths, kinds, flags=0) -> np.ndarray:
     """Host array of smol_csum_desc_t (view it as uint8 and copy it to the device)."""
     n = len(offsets)
     d = np.zeros(n, dtype=DESC_DTYPE)
     d["offset"] = np.asarray(offsets, dtype=np.uint64)
     d["len"] = np.asarray(lengths, dtype=np.uint32)
     d["kind"] = np.broadcast_to(np.asarray(kinds, dtype=np.uint8), (n,))
+    d["flags"] = np.broadcast_to(np.asarray(flags, dtype=np.uint8), (n,))
     return d
 
 
@@ -84,6 +86,7 @@ class Batch:
     length: int = 0
     kind: int = KIND_IP
     desc: Optional[object] = None  # torch.Tensor (uint8, device) holding n descriptors
+    flags: int = 0                 # SMOL_REC_* of every record of a fixed-stride batch
 
     def c(self) -> BatchC:
         b = BatchC()
@@ -92,17 +95,18 @@ class Batch:
         b.stride = self.stride
         b.len = self.length
         b.kind = self.kind
+        b.flags = self.flags
         return b
 
     @staticmethod
-    def fixed(n: int, stride: int, length: Optional[int] = None, kind: int = KIND_IP) -> "Batch":
-        return Batch(n=n, stride=stride, length=stride if length is None else length, kind=kind)
+    def fixed(n: int, stride: int, length: Optional[int] = None, kind: int = KIND_IP, flags: int = 0) -> "Batch":
+        return Batch(n=n, stride=stride, length=stride if length is None else length, kind=kind, flags=flags)
 
     @staticmethod
-    def from_records(offsets, lengths, kinds, device) -> "Batch":
+    def from_records(offsets, lengths, kinds, device, flags=0) -> "Batch":
         import torch
 
-        d = make_descriptors(offsets, lengths, kinds)
+        d = make_descriptors(offsets, lengths, kinds, flags)
         t = torch.from_numpy(d.view(np.uint8).copy()).to(device)
         return Batch(n=len(d), desc=t)
 

@@ -150,11 +150,12 @@ struct Batch {
     uint64_t stride = 0;
     uint32_t len = 0;
     Medium kind = Medium::Ip;
+    uint8_t flags = 0;  // SMOL_REC_* of every record (fixed stride; descriptors carry their own)
 
-    static Batch fixed(uint64_t n, uint64_t stride, uint32_t len, Medium kind = Medium::Ip) {
-        return Batch{nullptr, n, stride, len, kind};
+    static Batch fixed(uint64_t n, uint64_t stride, uint32_t len, Medium kind = Medium::Ip, uint8_t flags = 0) {
+        return Batch{nullptr, n, stride, len, kind, flags};
     }
-    static Batch described(const smol_csum_desc_t* d_desc, uint64_t n) { return Batch{d_desc, n, 0, 0, Medium::Ip}; }
+    static Batch described(const smol_csum_desc_t* d_desc, uint64_t n) { return Batch{d_desc, n, 0, 0, Medium::Ip, 0}; }
 
     smol_csum_batch_t c() const {
         smol_csum_batch_t b{};
@@ -163,6 +164,7 @@ struct Batch {
         b.stride = stride;
         b.len = len;
         b.kind = uint8_t(kind);
+        b.flags = flags;
         return b;
     }
 };

@@ -134,10 +134,10 @@ def pack(records, align: int = 1, gap_rng=None, base_pad: int = 0):
     return buf, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
 
 
-def oracle_desc(offs, lens, kinds):
+def oracle_desc(offs, lens, kinds, flags=0):
     from smoltcp_amd.engine import make_descriptors
 
-    return make_descriptors(offs, lens, kinds)
+    return make_descriptors(offs, lens, kinds, flags)
 
 
 def oracle_verify_records(buf, offs, lens, kinds, caps=(0, 0, 0, 0, 0)):

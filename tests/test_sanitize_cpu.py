@@ -79,6 +79,16 @@ def test_oracle_and_scalar_mirrors_asan_random(built, seed):
     assert r.stdout.strip() == "ok 20000"
 
 
+@pytest.mark.parametrize("seed", [3, 0xF4A6])
+def test_oracle_frag_groups_asan(built, seed):
+    """The fragment-group oracle (group_copy into its 128 KiB reassembly buffer, offsets up to
+    65528) and the dispatch_ip restatement under ASan/UBSan."""
+    r = subprocess.run([os.path.join(built, "oracle_asan"), "frag", str(seed), "3000"], capture_output=True,
+                       text=True, timeout=600, env=ENV)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.strip() == "ok 3000"
+
+
 def test_host_mirror_asan(built, tmp_path, golden):
     rng = np.random.default_rng(9)
     lines = []
