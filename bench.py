@@ -58,7 +58,7 @@ def parse_args(argv=None):
                     help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
     ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
     ap.add_argument("--variant", type=int, default=-1, help="force a kernel variant (tuning)")
-    ap.add_argument("--probe", action="store_true", help="also time the read-only stream probe")
+    ap.add_argument("--probe", action="store_true", help="(kept for old scripts: the probes always run)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch + rendezvous + reporting only, on CPU (gloo), no checksum work")
     return ap.parse_args(argv)
@@ -182,6 +182,12 @@ class Workload:
             eng.corrupt(self.rx, self.batch, every=64, seed=seed)
         self.status = torch.empty(self.n, dtype=torch.uint8, device=dev)
         self.est = None
+        # emit's floor probe: (record spacing, field offsets) — IPv4 header + UDP / TCP checksum;
+        # C4 one L4 field (UDP's offset; TCP's and ICMPv6's sit in the same first line); C3 at the
+        # mean record spacing (the same bytes and the same number of store events)
+        self.probe_fields = {"c2": (1500, 10, 26), "c5": (1500, 10, 26), "c2copy": (1500, 10, 26),
+                             "c4": (1320, 46, 0xFFFFFFFF),
+                             "c3": (max(16, self.total // max(self.n, 1)), 10, 36)}[cfg]
 
 
 # ---------------------------------------------------------------------------------------------
@@ -232,8 +238,8 @@ def _oracle_pass(oracle, tx, rx, desc, m, stride, L, kind, caps, threads, pool):
         oracle.batch_emit(tx, desc[lo:hi], hi - lo, 0, 0, kind, caps)
         return oracle.batch_verify(rx, desc[lo:hi], hi - lo, 0, 0, kind, caps)
 
-    if threads == 1:
-        return run(bounds[0])
+    if threads == 1:  # on a (pinned) worker thread too
+        return pool.submit(run, bounds[0]).result()
     return np.concatenate(list(pool.map(run, bounds)))
 
 
@@ -276,7 +282,24 @@ def cpu_baseline(E, wl, seconds: float):
     build = oracle.use_native()
     res = {}
     st = None
-    with cf.ThreadPoolExecutor(threads) as pool:
+    # every worker thread pinned to its own CPU of this process's affinity set (spread over it), so
+    # the scheduler does not migrate the threads between passes
+    aff = sorted(os.sched_getaffinity(0))
+    pin = [aff[(i * len(aff)) // threads] for i in range(threads)]
+    slot = iter(range(threads))
+    import threading
+    lock = threading.Lock()
+
+    def pin_worker():
+        with lock:
+            i = next(slot)
+        try:
+            os.sched_setaffinity(0, {pin[i]})  # Linux: pid 0 = the calling thread
+        except OSError:
+            pass
+
+    with cf.ThreadPoolExecutor(threads, initializer=pin_worker) as pool:
+        list(pool.map(lambda _: time.sleep(0.05), range(threads)))  # start (and pin) every worker
         for t in sorted({1, threads}):
             _oracle_pass(oracle, tx, rx, desc, m, stride, L, wl.kind, caps, t, pool)  # warm
             times, t0 = [], time.perf_counter()
@@ -285,8 +308,11 @@ def cpu_baseline(E, wl, seconds: float):
                 st = _oracle_pass(oracle, tx, rx, desc, m, stride, L, wl.kind, caps, t, pool)
                 times.append(time.perf_counter() - a)
             med, best = float(np.median(times)), float(min(times))
+            p10, p90 = (float(x) for x in np.percentile(times, [10, 90]))
             res[t] = {"GiB/s": 2 * span / med / GIB, "best_GiB/s": 2 * span / best / GIB, "reps": len(times),
-                      "median_s": med, "spread": float((max(times) - min(times)) / med)}
+                      "median_s": med, "spread": float((max(times) - min(times)) / med),
+                      "p10_p50_p90_GiB/s": [round(2 * span / x / GIB, 2) for x in (p90, med, p10)],
+                      "spread_p10_p90": float((p90 - p10) / med)}
     torch.cuda.synchronize()
     parity = {"records": m, "emit_bitexact": bool(np.array_equal(tx, dev_tx)),
               "verify_bitexact": bool(np.array_equal(st, dev_st)),
@@ -296,6 +322,10 @@ def cpu_baseline(E, wl, seconds: float):
            "single_core_value": round(res[1]["GiB/s"], 3),
            "best_value": round(r["best_GiB/s"], 3), "single_core_best_value": round(res[1]["best_GiB/s"], 3),
            "spread": round(r["spread"], 3),
+           "spread_p10_p90": round(r["spread_p10_p90"], 3),
+           "pass_rate_p10_p50_p90": r["p10_p50_p90_GiB/s"],
+           "single_core_pass_rate_p10_p50_p90": res[1]["p10_p50_p90_GiB/s"],
+           "pinned_cpus": pin,
            "host": share,
            "sample": f"{m} records of the same workload ({end / 1e9:.2f} GB per buffer, > host LLC): emit tx + "
                      f"verify rx; median of {r['reps']} passes on {threads} threads ({res[1]['reps']} on 1; the "
@@ -460,21 +490,36 @@ def main(argv=None):
     rejected = int(((st & E.ST_ACCEPT) == 0).sum())
     per = gather_floats([rank, local, mine, emit_ms, verify_ms, rejected], device=dev)
 
-    probe = None
-    if args.probe and rank == 0:
+    # Emit's floor (rank 0): the read-only stream probe over the TX buffer, and the same stream plus
+    # emit's scattered field stores (smol_csum_tool_field_probe: 2-B stores at the records' field
+    # offsets, one store event per field per record).  An in-place emit cannot beat the second.
+    probe = floor = None
+    if rank == 0 and wl.copy is None:
         sink = torch.zeros(1, dtype=torch.int32, device=dev)
-        for _ in range(3):
-            eng.stream_read(wl.rx, sink)
+
+        def timed(fn, reps=10):
+            for _ in range(3):
+                fn()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(reps):
+                fn()
+            b.record(stream)
+            torch.cuda.synchronize()
+            return a.elapsed_time(b) / reps
+
+        ro_ms = timed(lambda: eng.stream_read(wl.tx, sink, stream=stream))
+        stride, f1, f2 = wl.probe_fields
+        fp_ms = timed(lambda: eng.field_probe(wl.tx, stride, f1, f2, stream=stream))
+        eng.emit(wl.tx, wl.batch, stream=stream)  # the probe overwrote the fields: emit them again
         torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(10):
-            eng.stream_read(wl.rx, sink, stream=stream)
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms = a.elapsed_time(b) / 10
-        probe = {"kernel": "stream_read_kernel", "bytes": wl.rx.numel() // 16 * 16, "ms": round(ms, 4),
-                 "GB/s": round(wl.rx.numel() / ms / 1e6, 1)}
+        nbytes = wl.tx.numel() // 16 * 16
+        probe = {"kernel": "stream_read_kernel", "bytes": nbytes, "ms": round(ro_ms, 4),
+                 "GB/s": round(nbytes / ro_ms / 1e6, 1)}
+        floor = {"kernel": "field_probe_kernel", "ms": round(fp_ms, 4), "read_only_ms": round(ro_ms, 4),
+                 "what": f"the TX buffer streamed once (best read pattern) + a 2-B store at offsets {f1}"
+                         + (f" and {f2}" if f2 != 0xFFFFFFFF else "") + f" of every {stride}-B record "
+                         "(emit's store events, no parse / gates): the time an in-place emit cannot beat"}
 
     unfused = None
     if wl.copy is not None and rank == 0:
@@ -555,6 +600,9 @@ def main(argv=None):
         }
         if probe:
             out["stream_read_probe"] = probe
+        if floor and dom == "emit":
+            out["roofline"]["floor"] = floor
+            out["roofline"]["floor_frac"] = round(floor["ms"] / kd["ms"], 4)
         if unfused:
             out["unfused_tx"] = unfused
         print(json.dumps(out), flush=True)

@@ -35,6 +35,7 @@ TOOL_SYMBOLS = [
     "smol_csum_tool_synth", "smol_csum_tool_corrupt", "smol_csum_tool_set_shape",
     "smol_csum_tool_set_variant", "smol_csum_tool_set_tile",
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
+    "smol_csum_tool_field_probe",
     "smol_csum_tool_kernel_name",
 ]
 
@@ -136,6 +137,8 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_tool_set_max_blocks.restype = i32
     L.smol_csum_tool_stream_read.argtypes = [vp, vp, u64, vp, vp]
     L.smol_csum_tool_stream_read.restype = i32
+    L.smol_csum_tool_field_probe.argtypes = [vp, vp, u64, u64, ctypes.c_uint32, ctypes.c_uint32, vp]
+    L.smol_csum_tool_field_probe.restype = i32
     L.smol_csum_tool_auto_shape.argtypes = [u32, i32]
     L.smol_csum_tool_auto_shape.restype = i32
     L.smol_csum_tool_kernel_name.argtypes = [vp, i32, i32]

@@ -410,6 +410,16 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
     return e == hipSuccess ? SMOL_OK : hip_fail(e, "stream-read kernel launch");
 }
 
+int smol_csum_tool_field_probe(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, uint64_t stride,
+                               uint32_t f1, uint32_t f2, void* stream) {
+    if (!ctx || !d_buf || (bytes & 15u) || ((uintptr_t)d_buf & 15u) || stride == 0 || f1 == ~0u) return SMOL_EINVAL;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    hipError_t e = launch_field_probe(d_buf, bytes, stride, f1, f2, (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * 8u,
+                                      (hipStream_t)stream);
+    return e == hipSuccess ? SMOL_OK : hip_fail(e, "field-probe kernel launch");
+}
+
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
     const int v = auto_variant(MODE_VERIFY, has_desc != 0);
     return auto_shape(len, has_desc != 0, line_grid(v), v);

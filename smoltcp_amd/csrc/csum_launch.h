@@ -92,5 +92,7 @@ hipError_t launch_frag(int mode, const KParams& p, const smol_csum_frag_group_t*
                        hipStream_t s);
 hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t max_blocks,
                               hipStream_t s);
+hipError_t launch_field_probe(uint8_t* buf, uint64_t bytes, uint64_t stride, uint32_t f1, uint32_t f2,
+                              uint32_t max_blocks, hipStream_t s);
 
 }  // namespace smolcsum

@@ -240,4 +240,60 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink
     return hipGetLastError();
 }
 
+// Emit's floor probe: the read-only stream above over a batch's bytes, plus what emit writes — two
+// big-endian 2-byte stores per record (one when f2 == ~0u) at record offsets f1 / f2 of records
+// that start every `stride` bytes, each store issued by the wavefront that streamed the 8-KiB piece
+// holding the record's first byte, right after that piece's loads (the stored value depends on
+// them).  Reads every byte once at the best streaming pattern and makes exactly emit's scattered
+// store events, with no parse and no gates: the time an in-place emit cannot beat
+// (tools/probe_wr2.hip).
+__device__ __forceinline__ void probe_store(uint8_t* buf, uint64_t bytes, uint64_t a, uint32_t v) {
+    if (a + 2 <= bytes) {
+        __attribute__((address_space(1))) uint8_t* g = (__attribute__((address_space(1))) uint8_t*)(buf + a);
+        g[0] = (uint8_t)(v >> 8);
+        g[1] = (uint8_t)v;
+    }
+}
+
+__global__ __launch_bounds__(256) void field_probe_kernel(uint8_t* buf, uint64_t n16, uint64_t stride, uint32_t f1,
+                                                          uint32_t f2) {
+    constexpr int UNR = 8;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const uint64_t per = 64ull * UNR;
+    const uint64_t bytes = n16 * 16;
+    const u32x4s* q = reinterpret_cast<const u32x4s*>(buf);
+    auto stores = [&](uint64_t lo, uint64_t hi, uint32_t acc) {  // records starting in [lo, hi)
+        const uint64_t r0 = (lo + stride - 1) / stride;
+        for (uint64_t r = r0 + (uint64_t)lane; r * stride < hi; r += 64) {
+            probe_store(buf, bytes, r * stride + f1, acc + (uint32_t)r);
+            if (f2 != ~0u) probe_store(buf, bytes, r * stride + f2, acc ^ (uint32_t)r);
+        }
+    };
+    for (uint64_t base = w0 * per; base + per <= n16; base += nw * per) {
+        u32x4s v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) v[u] = __builtin_nontemporal_load(q + base + u * 64 + lane);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+            acc += __builtin_amdgcn_sad_u16(v[u].x, 0, 0) + __builtin_amdgcn_sad_u16(v[u].y, 0, 0) +
+                   __builtin_amdgcn_sad_u16(v[u].z, 0, 0) + __builtin_amdgcn_sad_u16(v[u].w, 0, 0);
+        stores(16 * base, 16 * (base + per), acc);
+    }
+    const uint64_t tail = n16 / per * per;
+    if (w0 == 0 && tail < n16) {
+        uint32_t acc = 0;
+        for (uint64_t i = tail + (uint64_t)lane; i < n16; i += 64) acc += q[i].x;
+        stores(16 * tail, bytes, acc);
+    }
+}
+
+hipError_t launch_field_probe(uint8_t* buf, uint64_t bytes, uint64_t stride, uint32_t f1, uint32_t f2,
+                              uint32_t max_blocks, hipStream_t s) {
+    hipLaunchKernelGGL(field_probe_kernel, dim3(max_blocks), dim3(256), 0, s, buf, bytes / 16, stride, f1, f2);
+    return hipGetLastError();
+}
+
 }  // namespace smolcsum

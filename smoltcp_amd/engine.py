@@ -284,6 +284,13 @@ class ChecksumEngine:
         check(lib().smol_csum_tool_stream_read(self._h, buf.data_ptr(), nbytes, sink.data_ptr(),
                                                self._stream(stream)), "smol_csum_tool_stream_read")
 
+    def field_probe(self, buf, stride: int, f1: int, f2: int = 0xFFFFFFFF, stream=None):
+        """Emit's floor probe (tooling, smol_csum_tool_field_probe): stream-read the buffer and store
+        2 bytes at offsets f1 / f2 of every `stride`-byte record.  Overwrites those bytes."""
+        nbytes = buf.numel() // 16 * 16
+        check(lib().smol_csum_tool_field_probe(self._h, buf.data_ptr(), nbytes, int(stride), int(f1), int(f2),
+                                               self._stream(stream)), "smol_csum_tool_field_probe")
+
     def set_shape(self, shape: int):
         check(lib().smol_csum_tool_set_shape(self._h, int(shape)), "smol_csum_tool_set_shape")
 

@@ -69,3 +69,26 @@ def test_host_cpu_share():
 
     s = bench.host_cpu_share()
     assert s["threads"] >= 1 and s["nproc"] >= 1 and s["threads"] <= s["affinity"]
+
+
+@pytest.mark.gpu
+def test_bench_gpu_contract():
+    """The real GPU path of the launcher: `--gpus 1` on the box, the JSON contract of the line
+    (BASELINE.json's metric, n_gpus, per_rank, roofline with the emit floor, the clock ramp)."""
+    r = _run(["--gpus", "1", "--config", "c2", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0",
+              "--ramp-ms", "50"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert d["metric"] == base["metric"] and d["unit"] == "GiB/s" and d["higher_is_better"] is True
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["dtype"] == "u8"
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["scaling"] == "weak"
+    assert [p["rank"] for p in d["per_rank"]] == [0]
+    rl = d["roofline"]
+    assert rl["bound"] == "hbm" and rl["unit"] == "GB/s" and rl["peak"] == 8000.0
+    assert 0 < rl["frac"] < 1 and abs(rl["achieved"] / rl["peak"] - rl["frac"]) < 1e-3
+    assert rl["floor"]["kernel"] == "field_probe_kernel" and 0 < rl["floor_frac"]
+    n64 = d["config"]["records_per_gpu"] // 64  # 1/64 single-bit flips (a few the gates cannot see)
+    assert d["ramp"]["steps"] >= 8 and n64 - 16 <= d["verify_rejected"] <= n64
+    assert d["cpu_baseline"] is None  # --cpu-seconds 0
