@@ -199,6 +199,24 @@ def test_copy_emit_mixed_packed(eng, shape, variant):
     assert (st & E.ST_MALFORMED).sum() == 0
 
 
+@pytest.mark.parametrize("variant", [-1, 16, 17])
+def test_copy_emit_packed_zero_gaps(eng, variant):
+    """C3-style batch: TCP records of U[64, 9000] bytes packed back to back with no gap (odd
+    offsets), so neighbouring records share cache lines.  Copy-emit rewrites every byte of a record
+    (include/smolcsum.h); a neighbour's bytes must survive bit for bit."""
+    rng = np.random.default_rng(17)
+    recs, spec = [], []
+    for i in range(1500):
+        L = int(rng.integers(64, 9001))
+        r = P.ipv4(V4A, V4B, 6, P.tcp(1000 + i % 5000, 80, P.rand_bytes(rng, L - 40)))
+        recs.append(r)
+        spec.append((40, L - 40) if i % 3 else (20 + int(rng.integers(0, 20)), L - 40))
+    st, got, offs, lens = _run(eng, recs, spec, seed=18, variant=variant)
+    assert (offs % 2 == 1).any() and not (st & E.ST_MALFORMED).any()
+    vst = P.oracle_verify_records(got.copy(), offs, lens, np.ones(len(recs), np.uint8))
+    assert (vst & E.ST_ACCEPT).all()
+
+
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 def test_copy_emit_all_alignments(eng, variant):
     """dst offsets and source offsets cover every residue mod 16."""

@@ -4,10 +4,11 @@
     rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 bench.py --steps K --warmup W --cpu-seconds 0
     python tools/step_trace.py DIR --steps K --warmup W [--out profiles/r03_step_trace_c2.json]
 
-bench.py launches, after the workload set-up, W warm-up steps, the K timed steps and K more steps
-with HIP events (the kernel-duration pass), each step = one emit (or copy-emit) + one verify.  The
-last 4K checksum launches of the trace are therefore the timed and the event pass, and the 2W
-before them the warm-up.  For every step this prints the emit and verify durations and the gaps
+bench.py launches, after the workload set-up, the clock-ramp steps, W warm-up steps, the K timed
+steps and K more steps with HIP events (the kernel-duration pass), each step = one emit (or
+copy-emit) + one verify; then the probes (stream_read_kernel first) and one more emit.  The last 4K
+checksum launches before the first probe kernel are therefore the timed and the event pass, and
+the 2W before them the warm-up.  For every step this prints the emit and verify durations and the gaps
 (emit start - previous verify end, verify start - emit end), and sums up the timed region: the
 kernel sum, the gaps and the span from the first timed kernel's start to the last one's end.
 """
@@ -28,13 +29,17 @@ def load(d):
     hits = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))
     if not hits:
         raise SystemExit(f"no kernel_trace.csv under {d}")
-    rows = []
+    rows, probes = [], []
     with open(hits[0]) as f:
         for r in csv.DictReader(f):
             role = kernel_role(r["Kernel_Name"])
             if role in ("emit", "verify", "copy_emit"):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), role))
+            elif "stream_read_kernel" in r["Kernel_Name"]:
+                probes.append(int(r["Start_Timestamp"]))
     rows.sort()
+    if probes:  # drop what bench.py runs after the event pass (the probes and the re-emit)
+        rows = [x for x in rows if x[0] < min(probes)]
     return rows
 
 
