@@ -222,6 +222,55 @@ def host_cpu_share() -> dict:
     return {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota, "threads": threads}
 
 
+def _cpulist(text: str):
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
+def pick_cpus(threads: int):
+    """`threads` CPUs of this process's affinity set for the CPU baseline: on the NUMA node the
+    process runs on, one hardware thread per core first (SMT siblings only when the node runs out),
+    then other nodes.  Returns (cpus, node)."""
+    aff = set(os.sched_getaffinity(0))
+    try:
+        with open("/proc/self/stat") as f:
+            cur = int(f.read().rsplit(")", 1)[1].split()[36])  # field 39: the CPU last run on
+    except (OSError, ValueError, IndexError):
+        cur = min(aff)
+    nodes = {}
+    for path in glob.glob("/sys/devices/system/node/node[0-9]*/cpulist"):
+        try:
+            with open(path) as f:
+                nodes[int(path.split("node")[-1].split("/")[0])] = [c for c in _cpulist(f.read()) if c in aff]
+        except (OSError, ValueError):
+            pass
+    if not nodes:
+        nodes = {0: sorted(aff)}
+    home = next((n for n, cs in nodes.items() if cur in cs), min(nodes))
+
+    def core(c):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                cid = int(f.read())
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                return int(f.read()), cid
+        except (OSError, ValueError):
+            return c, c
+
+    order = []
+    for n in [home] + sorted(k for k in nodes if k != home):
+        seen, firsts, rest = set(), [], []
+        for c in nodes[n]:
+            (rest if core(c) in seen else firsts).append(c)
+            seen.add(core(c))
+        order += firsts + rest
+    return order[:threads] or sorted(aff)[:threads], home
+
+
 def _oracle_pass(oracle, tx, rx, desc, m, stride, L, kind, caps, threads, pool):
     """One emit(tx) + verify(rx) pass of the oracle over m records, split over `threads` host
     threads (ctypes releases the GIL inside the C calls).  Returns the verify status array."""
@@ -260,6 +309,14 @@ def cpu_baseline(E, wl, seconds: float):
         return None, None
     share = host_cpu_share()
     threads = share["threads"]
+    # the baseline's threads: one per core on this process's NUMA node; the main thread moves there
+    # first, so the sample's host copies are first touched on that node's memory
+    pin, node = pick_cpus(threads)
+    main_aff = os.sched_getaffinity(0)
+    try:
+        os.sched_setaffinity(0, set(pin))
+    except OSError:
+        pass
     if wl.batch.desc is None:
         L = wl.batch.length
         m = min(wl.n, max(1, CPU_SAMPLE_BYTES // L))
@@ -282,10 +339,8 @@ def cpu_baseline(E, wl, seconds: float):
     build = oracle.use_native()
     res = {}
     st = None
-    # every worker thread pinned to its own CPU of this process's affinity set (spread over it), so
-    # the scheduler does not migrate the threads between passes
-    aff = sorted(os.sched_getaffinity(0))
-    pin = [aff[(i * len(aff)) // threads] for i in range(threads)]
+    # every worker thread pinned to its own CPU (pick_cpus), so the scheduler does not migrate the
+    # threads between passes
     slot = iter(range(threads))
     import threading
     lock = threading.Lock()
@@ -314,6 +369,10 @@ def cpu_baseline(E, wl, seconds: float):
                       "p10_p50_p90_GiB/s": [round(2 * span / x / GIB, 2) for x in (p90, med, p10)],
                       "spread_p10_p90": float((p90 - p10) / med)}
     torch.cuda.synchronize()
+    try:
+        os.sched_setaffinity(0, main_aff)
+    except OSError:
+        pass
     parity = {"records": m, "emit_bitexact": bool(np.array_equal(tx, dev_tx)),
               "verify_bitexact": bool(np.array_equal(st, dev_st)),
               "checker": "oracle/csum_oracle.c on the cpu_baseline sample"}
@@ -325,7 +384,7 @@ def cpu_baseline(E, wl, seconds: float):
            "spread_p10_p90": round(r["spread_p10_p90"], 3),
            "pass_rate_p10_p50_p90": r["p10_p50_p90_GiB/s"],
            "single_core_pass_rate_p10_p50_p90": res[1]["p10_p50_p90_GiB/s"],
-           "pinned_cpus": pin,
+           "pinned_cpus": pin, "numa_node": node,
            "host": share,
            "sample": f"{m} records of the same workload ({end / 1e9:.2f} GB per buffer, > host LLC): emit tx + "
                      f"verify rx; median of {r['reps']} passes on {threads} threads ({res[1]['reps']} on 1; the "
