@@ -52,6 +52,7 @@ namespace smolcsum {
 // (fixed-stride emit only: the 128-B line(s) holding the two fields stay resident in L2 when the
 // field stores arrive; measured in DESIGN.md §5).
 // 13 = variant 5 without the register prefetch.
+// 14 = variant 5 with shared boundary lines (shared_from) for fixed-stride VERIFY too.
 // MODE_COPY (16-byte grid, plain loads, no register prefetch): 8 = two aligned source chunks per
 // destination chunk; 11 = one, the second taken from the next lane of the group (DPP /
 // ds_bpermute); 16 (the default) = variant 11 with dword-aligned source loads — a lane loads the 16
@@ -60,9 +61,10 @@ namespace smolcsum {
 // the record written (WHOLE, see walk_step).  Measured variants that lost are in DESIGN.md §6.
 template <int VAR>
 struct VarT {
-    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13;
+    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 14;
     static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16;
-    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13;
+    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 14;
+    static constexpr bool SHV = VAR == 14;  // shared_from in verify
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
@@ -529,9 +531,9 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
 // window is used only when record r+1 is the neighbour's one and only record (the natural grid),
 // so that it is filled at the start and never overwritten.  Stride >= 384 keeps that line out of
 // record r's own window.
-template <int G, int MODE, bool IMPLICIT, bool LINE>
+template <int G, int MODE, bool IMPLICIT, bool LINE, bool SHV = false>
 __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, uint64_t a0, int gib, uint64_t ngroups) {
-    constexpr bool SHARE = IMPLICIT && LINE && MODE == MODE_EMIT;
+    constexpr bool SHARE = IMPLICIT && LINE && (MODE == MODE_EMIT || (SHV && MODE == MODE_VERIFY));
     constexpr int GPW = 64 / G;  // groups per wavefront
     if (!SHARE || p.stride < 384 || (gib % GPW) == GPW - 1 || r + 1 >= p.n || r + 1 >= ngroups ||
         r + 1 + ngroups < p.n)
@@ -542,7 +544,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
-          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false>
+          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false, bool SHV = false>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib) {
@@ -565,7 +567,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     // every record's last step would otherwise issue U loads of the dummy line)
     if (PF && (!SKIPD || have2))
         load_step<G, U, NT, COPY, LINE, CU, SHUF, SHUF2>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
-                                            shared_from<G, MODE, IMPLICIT, LINE>(p, r2, rec2.a0, gib, ngroups));
+                                            shared_from<G, MODE, IMPLICIT, LINE, SHV>(p, r2, rec2.a0, gib, ngroups));
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
@@ -757,7 +759,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 
     // ---- sum this step's chunks over [0, s1) (data: [0, len)) ----
     const int s1 = w.s1;
-    const uint64_t lim = shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups);
+    const uint64_t lim = shared_from<G, MODE, IMPLICIT, LINE, SHV>(p, w.r, w.cur.a0, gib, ngroups);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t k = w.step * (G * U) + u * G + lane;
@@ -846,6 +848,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool SHUF = VarT<VAR>::SHUF;
     constexpr bool WHOLE = VarT<VAR>::WHOLE;
     constexpr bool SHUF2 = VarT<VAR>::SHUF2;
+    constexpr bool SHV = VarT<VAR>::SHV;
     // Fixed-stride batches: no prefetch once the group has nothing left (one record per group in
     // a natural grid), measured 1-1.5 % faster (C2 verify 0.2444 -> 0.2422 ms, C4 0.2219 -> 0.2189
     // ms).  Descriptor batches keep the unconditional prefetch: there the conditional load made
@@ -881,11 +884,11 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     if (PF) {
         Regs<U, COPY> vb;
         load_step<G, U, NT, COPY, LINE, CU, SHUF>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
-                                                  shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
+                                                  shared_from<G, MODE, IMPLICIT, LINE, SHV>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF>(p, w, va, vb, lane, ngroups, &win[gib][0], gib)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF>(p, w, vb, va, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SHV>(p, w, va, vb, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SHV>(p, w, vb, va, lane, ngroups, &win[gib][0], gib)) break;
         }
     } else {
         while (true) {
@@ -934,7 +937,11 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
         case 9:
         case 10:
-            if constexpr (MODE == MODE_EMIT && IMPLICIT) {
+        case 14:
+            // fixed-stride emit / verify experiments: cached field lines (9, 10),
+            // shared boundary lines in verify (14)
+            if constexpr ((MODE == MODE_EMIT || MODE == MODE_VERIFY) && IMPLICIT) {
+                if (var == 14) return launch_shape<MODE, IMPLICIT, MODE == MODE_VERIFY ? 14 : 5>(shape, p, max_blocks, s);
                 return var == 9 ? launch_shape<MODE, IMPLICIT, 9>(shape, p, max_blocks, s)
                                 : launch_shape<MODE, IMPLICIT, 10>(shape, p, max_blocks, s);
             }

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--blocks", default="0")
     ap.add_argument("--var", default="0,1,2")
     ap.add_argument("--tile", default="32")
+    ap.add_argument("--rounds", type=int, default=2)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     eng = E.ChecksumEngine(0)
@@ -35,7 +36,14 @@ def main():
     s = torch.cuda.current_stream(dev)
     rows = []
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    for rnd in range(2):
+    import time
+    t0 = time.perf_counter()  # clock ramp (bench.py --ramp-ms): 0.3 s of steps before timing
+    while time.perf_counter() - t0 < 0.3:
+        for _ in range(8):
+            eng.emit(wl.tx, wl.batch, stream=s)
+            eng.verify(wl.rx, wl.batch, status=wl.status, stream=s)
+        torch.cuda.synchronize()
+    for rnd in range(args.rounds):
         for shape in [int(x) for x in args.shapes.split(",")]:
             for var, bpc, tile in [(a, b, d) for a in [int(x) for x in args.var.split(",")]
                                    for b in [int(x) for x in args.blocks.split(",")]
