@@ -23,6 +23,12 @@ def main():
     src = torch.randint(0, 256, (n * 1472 + 16,), dtype=torch.uint8, device=dev)
     cp = torch.from_numpy(E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472).view(np.uint8).copy()).to(dev)
     variants = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "-1").split(",")]
+    import time
+    t0 = time.perf_counter()  # clock ramp (bench.py --ramp-ms)
+    while time.perf_counter() - t0 < 0.3:
+        for _ in range(8):
+            eng.copy_emit(tx, b, src, cp)
+        torch.cuda.synchronize()
     shapes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,3,5").split(",")]
     for rnd, shape, var in [(r, s, v) for r in range(3) for s in shapes for v in variants]:
         eng.set_shape(shape)
