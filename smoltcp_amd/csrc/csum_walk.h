@@ -956,7 +956,8 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
 template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
-    if (var == 5 || var == 6) {
+    // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 14) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
