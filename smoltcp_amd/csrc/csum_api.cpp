@@ -93,7 +93,7 @@ int walk_variant(int mode, bool has_desc) {
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
-bool line_grid(int variant) { return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 14; }
+bool line_grid(int variant) { return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 14 || variant == 15; }
 
 int auto_shape(uint32_t len, bool has_desc, bool line = false, int variant = -1) {
     if (has_desc) return variant == 13 ? CFG_G16U4 : CFG_G16U3;
@@ -382,7 +382,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 17) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 20) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

@@ -53,6 +53,8 @@ namespace smolcsum {
 // field stores arrive; measured in DESIGN.md §5).
 // 13 = variant 5 without the register prefetch.
 // 14 = variant 5 with shared boundary lines (shared_from) for fixed-stride VERIFY too.
+// 15 = variant 5 with the group's first step (its first record's first line, in the natural grid
+// the record's only step 0) loaded cached: the neighbour's last step then finds that line in L2.
 // MODE_COPY (16-byte grid, plain loads, no register prefetch): 8 = two aligned source chunks per
 // destination chunk; 11 = one, the second taken from the next lane of the group (DPP /
 // ds_bpermute); 16 (the default) = variant 11 with dword-aligned source loads — a lane loads the 16
@@ -61,9 +63,10 @@ namespace smolcsum {
 // the record written (WHOLE, see walk_step).  Measured variants that lost are in DESIGN.md §6.
 template <int VAR>
 struct VarT {
-    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 14;
+    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 14 || VAR == 15;
     static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16;
-    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 14;
+    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 14 || VAR == 15;
+    static constexpr int CU_FIRST = VAR == 15 ? 1 : 0;  // cached chunks per lane in the group's first step
     static constexpr bool SHV = VAR == 14;  // shared_from in verify
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
@@ -849,6 +852,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool WHOLE = VarT<VAR>::WHOLE;
     constexpr bool SHUF2 = VarT<VAR>::SHUF2;
     constexpr bool SHV = VarT<VAR>::SHV;
+    constexpr int CU0 = VarT<VAR>::CU_FIRST ? VarT<VAR>::CU_FIRST : CU;  // the first step's cached chunks
     // Fixed-stride batches: no prefetch once the group has nothing left (one record per group in
     // a natural grid), measured 1-1.5 % faster (C2 verify 0.2444 -> 0.2422 ms, C4 0.2219 -> 0.2189
     // ms).  Descriptor batches keep the unconditional prefetch: there the conditional load made
@@ -883,7 +887,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     Regs<U, COPY> va;
     if (PF) {
         Regs<U, COPY> vb;
-        load_step<G, U, NT, COPY, LINE, CU, SHUF>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
+        load_step<G, U, NT, COPY, LINE, CU0, SHUF>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
                                                   shared_from<G, MODE, IMPLICIT, LINE, SHV>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
@@ -938,10 +942,12 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 9:
         case 10:
         case 14:
+        case 15:
             // fixed-stride emit / verify experiments: cached field lines (9, 10),
             // shared boundary lines in verify (14)
             if constexpr ((MODE == MODE_EMIT || MODE == MODE_VERIFY) && IMPLICIT) {
                 if (var == 14) return launch_shape<MODE, IMPLICIT, MODE == MODE_VERIFY ? 14 : 5>(shape, p, max_blocks, s);
+                if (var == 15) return launch_shape<MODE, IMPLICIT, 15>(shape, p, max_blocks, s);
                 return var == 9 ? launch_shape<MODE, IMPLICIT, 9>(shape, p, max_blocks, s)
                                 : launch_shape<MODE, IMPLICIT, 10>(shape, p, max_blocks, s);
             }
@@ -957,7 +963,7 @@ template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
     // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
-    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 14) {
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 14 || var == 15) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
