@@ -93,11 +93,10 @@ int walk_variant(int mode, bool has_desc) {
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
-bool line_grid(int variant) { return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 14 || variant == 15 ||
-                                     variant == 21 || variant == 22; }
+bool line_grid(int variant) { return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13; }
 
 int auto_shape(uint32_t len, bool has_desc, bool line = false, int variant = -1) {
-    if (has_desc) return (variant == 13 || variant == 22) ? CFG_G16U4 : CFG_G16U3;
+    if (has_desc) return variant == 13 ? CFG_G16U4 : CFG_G16U3;
     const uint64_t need = (uint64_t)len + (line ? 127 : 15);  // bytes of aligned chunks a record can touch
     // eight records per wavefront in two steps, with as few idle lanes as possible (C4's 1320-B
     // records on the line grid: 8 x 6 0.2083 ms, 8 x 7 0.2188 ms; C2's 1500 B: 8 x 7 0.2327 ms)
@@ -167,7 +166,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         // chunks): C2copy 0.772-0.853 ms (variant 16) -> 0.689 ms (tools/exp_copy.py, MI355X).
         // Variants 1 / 8 / 11 / 16 stay selectable.
         const int cv = ctx->variant;
-        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || (cv >= 18 && cv <= 20)) ? cv : 17;
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? cv : 17;
         const int cshape = ctx->shape >= 0 ? ctx->shape : (var == 17 ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
@@ -383,7 +382,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 22) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 17) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

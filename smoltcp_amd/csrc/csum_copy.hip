@@ -68,11 +68,7 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 
 }  // namespace copy2
 
-// OPT (experiments): bit 0 = no destination load for a generic chunk whose record
-// bytes all lie in the copy range (the record's last chunk: its other bytes belong to the next
-// record and are neither summed nor stored); bit 1 = the window chunks that hold no field are
-// stored in round 1, only the field chunks after the gates.
-template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0, int OPT = 0>
+template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0>
 __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
     constexpr int GPB = 256 / G;
@@ -131,10 +127,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             const int lo = (int)rr.p0 - pos, hi = (int)rr.p1 - pos;
             const bool full = lo <= 0 && hi >= 16;
             const bool any = pay && lo < 16 && hi > 0;
-            // OPT & 1: the record's bytes of the chunk all come from the source
-            const int rlo = pos > 0 ? pos : 0, rhi = pos + 16 < (int)rr.len ? pos + 16 : (int)rr.len;
-            const bool covered = (OPT & 1) && pay && (int)rr.p0 <= rlo && rhi <= (int)rr.p1;
-            d = ld16<false>((gcv4)(in && !(pay && full) && !covered ? base + 16ull * k : dummy));
+            d = ld16<false>((gcv4)(in && !(pay && full) ? base + 16ull * k : dummy));
             const uint64_t sA = (sk + 16ull * k) & ~15ull;
             const uint64_t a0 = sA < first ? first : sA > last ? last : sA;
             const uint64_t a1 = sA + 16 < first ? first : sA + 16 > last ? last : sA + 16;
@@ -242,18 +235,6 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         }
         const bool far = f0b != NOF || f1b != NOF || f2b != NOF;
         const int len = (int)rr.len;
-        // OPT & 2: record offsets of the fields inside the window (the chunks holding one are stored
-        // after the gates; the others right away)
-        int wf0 = NOF, wf1 = NOF, wf2 = NOF;
-        if constexpr ((OPT & 2) != 0) {
-            wf0 = g.fam == 4 ? (int)g.ip_off + 10 : NOF;
-            wf1 = l4 ? (int)(g.l4_off + g.fo) : NOF;
-            wf2 = g.in_off ? (int)g.in_off + 10 : NOF;
-        }
-        auto field_in = [&](int pos) {
-            return (wf0 - pos > -2 && wf0 - pos < 16) || (wf1 - pos > -2 && wf1 - pos < 16) ||
-                   (wf2 - pos > -2 && wf2 - pos < 16);
-        };
 
         // ---- sum round 1; store its chunks past the window ----
         uint32_t acc = 0;
@@ -266,8 +247,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             if (in) {
                 const int pos = (int)(16u * k) - (int)head;
                 acc = sum_chunk(gm[u], pos, s1, acc);
-                if (!w || ((OPT & 2) && !field_in(pos)))
-                    store_part((gu8)base + 16u * k, gm[u], -pos, len - pos, f0b - pos, f1b - pos, f2b - pos);
+                if (!w) store_part((gu8)base + 16u * k, gm[u], -pos, len - pos, f0b - pos, f1b - pos, f2b - pos);
             }
         }
         // generic chunks beyond round 1 (a copy range that starts or ends far from the record's edges)
@@ -321,18 +301,18 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         wave_lds_sync();
         for (uint32_t k = (uint32_t)lane; k < (uint32_t)WIN_CH && k < nch; k += G) {
             const int pos = (int)(16u * k) - (int)head;
-            if (!(OPT & 2) || field_in(pos)) store_part((gu8)base + 16u * k, wn[k], -pos, len - pos, NOF, NOF, NOF);
+            store_part((gu8)base + 16u * k, wn[k], -pos, len - pos, NOF, NOF, NOF);
         }
         wave_lds_sync();  // the window is rewritten by the group's next record
     }
 }
 
-template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0, int OPT = 0>
+template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0>
 hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB, OPT>), dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -360,17 +340,7 @@ hipError_t launch_copy2(int shape, const KParams& p, uint32_t max_blocks, hipStr
     }
 }
 
-// variants 18 / 19 / 20: the default shape with OPT 1 / 2 / 3 (experiments)
-template <bool IMPLICIT>
-hipError_t launch_copy2_opt(int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    if (var == 18) return launch_copy2_one<IMPLICIT, 16, 4, 1, 2, 1>(p, max_blocks, s);
-    if (var == 19) return launch_copy2_one<IMPLICIT, 16, 4, 1, 2, 2>(p, max_blocks, s);
-    return launch_copy2_one<IMPLICIT, 16, 4, 1, 2, 3>(p, max_blocks, s);
-}
-
-hipError_t launch_copy_v17(int var, int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    if (var >= 18 && var <= 20)
-        return p.desc == nullptr ? launch_copy2_opt<true>(var, p, max_blocks, s) : launch_copy2_opt<false>(var, p, max_blocks, s);
+hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     return p.desc == nullptr ? launch_copy2<true>(shape, p, max_blocks, s) : launch_copy2<false>(shape, p, max_blocks, s);
 }
 

@@ -52,11 +52,6 @@ namespace smolcsum {
 // (fixed-stride emit only: the 128-B line(s) holding the two fields stay resident in L2 when the
 // field stores arrive; measured in DESIGN.md §5).
 // 13 = variant 5 without the register prefetch.
-// 14 = variant 5 with shared boundary lines (shared_from) for fixed-stride VERIFY too.
-// 21 / 22 = variant 5 / 13 with the chunks past the LDS window walked from the record's end (REV,
-// see rev_chunk), verify only.
-// 15 = variant 5 with the group's first step (its first record's first line, in the natural grid
-// the record's only step 0) loaded cached: the neighbour's last step then finds that line in L2.
 // MODE_COPY (16-byte grid, plain loads, no register prefetch): 8 = two aligned source chunks per
 // destination chunk; 11 = one, the second taken from the next lane of the group (DPP /
 // ds_bpermute); 16 (the default) = variant 11 with dword-aligned source loads — a lane loads the 16
@@ -65,14 +60,9 @@ namespace smolcsum {
 // the record written (WHOLE, see walk_step).  Measured variants that lost are in DESIGN.md §6.
 template <int VAR>
 struct VarT {
-    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 14 ||
-                               VAR == 15 || VAR == 21 || VAR == 22;
-    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 22;
-    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 14 || VAR == 15 ||
-                                 VAR == 21 || VAR == 22;
-    static constexpr int CU_FIRST = VAR == 15 ? 1 : 0;  // cached chunks per lane in the group's first step
-    static constexpr bool REV = VAR == 21 || VAR == 22;
-    static constexpr bool SHV = VAR == 14;  // shared_from in verify
+    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13;
+    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16;
+    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13;
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
@@ -146,17 +136,6 @@ __device__ __forceinline__ uint32_t n_chunks(const RecRef& rr) {
     return (uint32_t)(((rr.a0 + rr.len + 15) >> 4) - ((rr.a0 & ~(Grid<LINE>::ALIGN - 1)) >> 4));
 }
 
-// REV: the record's chunk in step slot k.  The window chunks keep their slots; the others are taken
-// from the record's END backwards, so that the record's last line — the next record's first — is
-// requested in step 0, right when the next record's group requests it for its LDS window.  The
-// two requests meet in L2 and the line comes from HBM once (with the natural order the last line
-// is requested one or two steps later and, loaded non-temporally, fetched again).
-template <bool REV, int WIN_CH>
-__device__ __forceinline__ uint32_t chunk_of(uint32_t k, uint32_t nch) {
-    if (!REV || k < (uint32_t)WIN_CH || nch <= (uint32_t)WIN_CH) return k;
-    return (uint32_t)WIN_CH + (nch - 1u - k);
-}
-
 template <bool NT>
 __device__ __forceinline__ u32x4 ld16(gcv4 q) {
     if (NT) return __builtin_nontemporal_load(q);
@@ -189,8 +168,7 @@ struct Regs<U, true> {
 // [A, A + 16) lies inside the source range's aligned chunks [first, last + 16); otherwise (the
 // payload's first / last chunk) at first / last, and the merge shifts it there.  Lane 0 also loads
 // the dword at A of the chunk after the step (sx1), for the group's last lane.
-template <int G, int U, bool NT, bool COPY, bool LINE, int CACHED_U = 0, bool SHUF = false, bool SHUF2 = false,
-          bool REV = false>
+template <int G, int U, bool NT, bool COPY, bool LINE, int CACHED_U = 0, bool SHUF = false, bool SHUF2 = false>
 __device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, uint32_t nch,
                                           uint32_t step, int lane, bool valid, uint64_t dummy,
                                           uint64_t lim = ~0ull) {
@@ -238,7 +216,7 @@ __device__ __forceinline__ void load_step(Regs<U, COPY>& R, const RecRef& rr, ui
         const uint32_t k = step * (G * U) + u * G + lane;
         const bool in = valid && k < nch && base + 16ull * k < lim;
         if constexpr (!COPY) {
-            const gcv4 q = (gcv4)(in ? base + 16ull * chunk_of<REV, Grid<LINE>::WIN_CH>(k, nch) : dummy);
+            const gcv4 q = (gcv4)(in ? base + 16ull * k : dummy);
             R.v[u] = u < CACHED_U ? ld16<false>(q) : ld16<NT>(q);  // folds per unrolled u
         } else {
             const int64_t pos = (int64_t)(16u * k) - (int64_t)(rr.a0 & 15u);  // record offset of the chunk
@@ -551,9 +529,9 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
 // window is used only when record r+1 is the neighbour's one and only record (the natural grid),
 // so that it is filled at the start and never overwritten.  Stride >= 384 keeps that line out of
 // record r's own window.
-template <int G, int MODE, bool IMPLICIT, bool LINE, bool SHV = false>
+template <int G, int MODE, bool IMPLICIT, bool LINE>
 __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, uint64_t a0, int gib, uint64_t ngroups) {
-    constexpr bool SHARE = IMPLICIT && LINE && (MODE == MODE_EMIT || (SHV && MODE == MODE_VERIFY));
+    constexpr bool SHARE = IMPLICIT && LINE && MODE == MODE_EMIT;
     constexpr int GPW = 64 / G;  // groups per wavefront
     if (!SHARE || p.stride < 384 || (gib % GPW) == GPW - 1 || r + 1 >= p.n || r + 1 >= ngroups ||
         r + 1 + ngroups < p.n)
@@ -564,7 +542,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
-          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false, bool SHV = false, bool REV = false>
+          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib) {
@@ -586,8 +564,8 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     // SKIPD: no prefetch when the group has nothing left (one record per group in a natural grid:
     // every record's last step would otherwise issue U loads of the dummy line)
     if (PF && (!SKIPD || have2))
-        load_step<G, U, NT, COPY, LINE, CU, SHUF, SHUF2, REV>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
-                                            shared_from<G, MODE, IMPLICIT, LINE, SHV>(p, r2, rec2.a0, gib, ngroups));
+        load_step<G, U, NT, COPY, LINE, CU, SHUF, SHUF2>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
+                                            shared_from<G, MODE, IMPLICIT, LINE>(p, r2, rec2.a0, gib, ngroups));
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
@@ -779,13 +757,12 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 
     // ---- sum this step's chunks over [0, s1) (data: [0, len)) ----
     const int s1 = w.s1;
-    const uint64_t lim = shared_from<G, MODE, IMPLICIT, LINE, SHV>(p, w.r, w.cur.a0, gib, ngroups);
+    const uint64_t lim = shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const uint32_t ks = w.step * (G * U) + u * G + lane;
-        const uint32_t k = chunk_of<REV, WIN_CH>(ks, w.nch);
+        const uint32_t k = w.step * (G * U) + u * G + lane;
         const int pos = (int)(16u * k) - (int)head;  // chunk start relative to the record
-        if (ks < w.nch && pos < s1 && pos + 16 > 0) {
+        if (k < w.nch && pos < s1 && pos + 16 > 0) {
             const uint64_t ca = base + 16ull * k;
             const u32x4 c = ca >= lim ? win[WIN_CH + ((ca - lim) >> 4)] : cm[u];  // neighbour's window
             if (pos < 0 || pos + 16 > s1) {  // first chunk (bytes before the record) / tail
@@ -869,9 +846,6 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     constexpr bool SHUF = VarT<VAR>::SHUF;
     constexpr bool WHOLE = VarT<VAR>::WHOLE;
     constexpr bool SHUF2 = VarT<VAR>::SHUF2;
-    constexpr bool SHV = VarT<VAR>::SHV;
-    constexpr bool REV = VarT<VAR>::REV;
-    constexpr int CU0 = VarT<VAR>::CU_FIRST ? VarT<VAR>::CU_FIRST : CU;  // the first step's cached chunks
     // Fixed-stride batches: no prefetch once the group has nothing left (one record per group in
     // a natural grid), measured 1-1.5 % faster (C2 verify 0.2444 -> 0.2422 ms, C4 0.2219 -> 0.2189
     // ms).  Descriptor batches keep the unconditional prefetch: there the conditional load made
@@ -906,18 +880,18 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     Regs<U, COPY> va;
     if (PF) {
         Regs<U, COPY> vb;
-        load_step<G, U, NT, COPY, LINE, CU0, SHUF, false, REV>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
-                                                  shared_from<G, MODE, IMPLICIT, LINE, SHV>(p, w.r, w.cur.a0, gib, ngroups));
+        load_step<G, U, NT, COPY, LINE, CU, SHUF>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
+                                                  shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SHV, REV>(p, w, va, vb, lane, ngroups, &win[gib][0], gib)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SHV, REV>(p, w, vb, va, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF>(p, w, va, vb, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF>(p, w, vb, va, lane, ngroups, &win[gib][0], gib)) break;
         }
     } else {
         while (true) {
-            load_step<G, U, NT, COPY, LINE, 0, SHUF, SHUF2, REV>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
+            load_step<G, U, NT, COPY, LINE, 0, SHUF, SHUF2>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
                                                             shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF, WHOLE, SHUF2, false, REV>(p, w, va, va, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF, WHOLE, SHUF2>(p, w, va, va, lane, ngroups, &win[gib][0], gib)) break;
         }
     }
 }
@@ -958,22 +932,9 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 5: return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
         case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
-        case 21:
-        case 22:  // REV: verify only (the other modes run the same variant without it)
-            if constexpr (MODE == MODE_VERIFY) {
-                return var == 21 ? launch_shape<MODE, IMPLICIT, 21>(shape, p, max_blocks, s)
-                                 : launch_shape<MODE, IMPLICIT, 22>(shape, p, max_blocks, s);
-            }
-            return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 9:
         case 10:
-        case 14:
-        case 15:
-            // fixed-stride emit / verify experiments: cached field lines (9, 10),
-            // shared boundary lines in verify (14)
-            if constexpr ((MODE == MODE_EMIT || MODE == MODE_VERIFY) && IMPLICIT) {
-                if (var == 14) return launch_shape<MODE, IMPLICIT, MODE == MODE_VERIFY ? 14 : 5>(shape, p, max_blocks, s);
-                if (var == 15) return launch_shape<MODE, IMPLICIT, 15>(shape, p, max_blocks, s);
+            if constexpr (MODE == MODE_EMIT && IMPLICIT) {
                 return var == 9 ? launch_shape<MODE, IMPLICIT, 9>(shape, p, max_blocks, s)
                                 : launch_shape<MODE, IMPLICIT, 10>(shape, p, max_blocks, s);
             }
@@ -989,7 +950,7 @@ template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
     // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
-    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 14 || var == 15 || var == 21 || var == 22) {
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
@@ -1020,15 +981,12 @@ hipError_t launch_copy_var(int shape, const KParams& p, uint32_t max_blocks, hip
 }
 
 // variant 17: the class-split copy-emit kernel (csum_copy.hip)
-hipError_t launch_copy_v17(int var, int shape, const KParams& p, uint32_t max_blocks, hipStream_t s);
+hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s);
 
 template <bool IMPLICIT>
 hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (var) {
-        case 17:
-        case 18:
-        case 19:
-        case 20: return launch_copy_v17(var, shape, p, max_blocks, s);
+        case 17: return launch_copy_v17(shape, p, max_blocks, s);
         case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
         case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);
         case 8: return launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);
