@@ -232,25 +232,21 @@ def _cpulist(text: str):
 
 
 def pick_cpus(threads: int):
-    """`threads` CPUs of this process's affinity set for the CPU baseline: on the NUMA node the
-    process runs on, one hardware thread per core first (SMT siblings only when the node runs out),
-    then other nodes.  Returns (cpus, node)."""
+    """`threads` CPUs of this process's affinity set for the CPU baseline: one hardware thread per
+    core (SMT siblings only once every core has one), taken round-robin over the NUMA nodes so that
+    every node's memory controllers serve the threads placed on it.  Returns (cpus, node of each)."""
     aff = set(os.sched_getaffinity(0))
-    try:
-        with open("/proc/self/stat") as f:
-            cur = int(f.read().rsplit(")", 1)[1].split()[36])  # field 39: the CPU last run on
-    except (OSError, ValueError, IndexError):
-        cur = min(aff)
     nodes = {}
     for path in glob.glob("/sys/devices/system/node/node[0-9]*/cpulist"):
         try:
             with open(path) as f:
-                nodes[int(path.split("node")[-1].split("/")[0])] = [c for c in _cpulist(f.read()) if c in aff]
+                cs = [c for c in _cpulist(f.read()) if c in aff]
+            if cs:
+                nodes[int(path.split("node")[-1].split("/")[0])] = cs
         except (OSError, ValueError):
             pass
     if not nodes:
         nodes = {0: sorted(aff)}
-    home = next((n for n, cs in nodes.items() if cur in cs), min(nodes))
 
     def core(c):
         try:
@@ -261,35 +257,68 @@ def pick_cpus(threads: int):
         except (OSError, ValueError):
             return c, c
 
-    order = []
-    for n in [home] + sorted(k for k in nodes if k != home):
+    per_node = {}
+    for n, cs in nodes.items():  # first hardware thread of each core, then the siblings
         seen, firsts, rest = set(), [], []
-        for c in nodes[n]:
+        for c in cs:
             (rest if core(c) in seen else firsts).append(c)
             seen.add(core(c))
-        order += firsts + rest
-    return order[:threads] or sorted(aff)[:threads], home
+        per_node[n] = firsts + rest
+    order, i = [], 0
+    while len(order) < threads and any(per_node.values()):
+        for n in sorted(per_node):
+            if per_node[n] and len(order) < threads:
+                order.append((per_node[n].pop(0), n))
+        i += 1
+    order = order or [(c, 0) for c in sorted(aff)[:threads]]
+    return [c for c, _ in order], [n for _, n in order]
 
 
-def _oracle_pass(oracle, tx, rx, desc, m, stride, L, kind, caps, threads, pool):
-    """One emit(tx) + verify(rx) pass of the oracle over m records, split over `threads` host
-    threads (ctypes releases the GIL inside the C calls).  Returns the verify status array."""
-    bounds = [S.shard_range(m, t, threads) for t in range(threads)]
+class PinnedTeam:
+    """`len(cpus)` host threads, thread i pinned to cpus[i] (Linux: sched_setaffinity(0) sets the
+    calling thread's mask), running one job at a time: run(fn) calls fn(i) on every thread i and
+    returns the results.  Memory a thread allocates and touches first lives on its NUMA node."""
 
-    def run(lo_hi):
-        lo, hi = lo_hi
-        if hi == lo:
-            return np.zeros(0, np.uint8)
-        if desc is None:
-            a, b = lo * stride, (hi - 1) * stride + L
-            oracle.batch_emit(tx[a:b], None, hi - lo, stride, L, kind, caps)
-            return oracle.batch_verify(rx[a:b], None, hi - lo, stride, L, kind, caps)
-        oracle.batch_emit(tx, desc[lo:hi], hi - lo, 0, 0, kind, caps)
-        return oracle.batch_verify(rx, desc[lo:hi], hi - lo, 0, 0, kind, caps)
+    def __init__(self, cpus):
+        import threading
 
-    if threads == 1:  # on a (pinned) worker thread too
-        return pool.submit(run, bounds[0]).result()
-    return np.concatenate(list(pool.map(run, bounds)))
+        self.n = len(cpus)
+        self.fn, self.out, self.stop = None, [None] * self.n, False
+        self.go = threading.Barrier(self.n + 1)
+        self.done = threading.Barrier(self.n + 1)
+        self.threads = [threading.Thread(target=self._loop, args=(i, c), daemon=True) for i, c in enumerate(cpus)]
+        for t in self.threads:
+            t.start()
+
+    def _loop(self, i, cpu):
+        try:
+            os.sched_setaffinity(0, {cpu})
+        except OSError:
+            pass
+        while True:
+            self.go.wait()
+            if self.stop:
+                return
+            try:
+                self.out[i] = self.fn(i)
+            except BaseException as e:  # re-raised by run()
+                self.out[i] = e
+            self.done.wait()
+
+    def run(self, fn):
+        self.fn = fn
+        self.go.wait()
+        self.done.wait()
+        for r in self.out:
+            if isinstance(r, BaseException):
+                raise r
+        return list(self.out)
+
+    def close(self):
+        self.stop = True
+        self.go.wait()
+        for t in self.threads:
+            t.join()
 
 
 def cpu_baseline(E, wl, seconds: float):
@@ -299,8 +328,6 @@ def cpu_baseline(E, wl, seconds: float):
     the value is the median of >= 10 passes.  The oracle is also the checker here: its emit of the
     sample (emit is idempotent) must reproduce the device's emitted bytes and its verify the
     device's status bytes, bit for bit."""
-    import concurrent.futures as cf
-
     import torch
 
     import oracle
@@ -309,14 +336,9 @@ def cpu_baseline(E, wl, seconds: float):
         return None, None
     share = host_cpu_share()
     threads = share["threads"]
-    # the baseline's threads: one per core on this process's NUMA node; the main thread moves there
-    # first, so the sample's host copies are first touched on that node's memory
-    pin, node = pick_cpus(threads)
-    main_aff = os.sched_getaffinity(0)
-    try:
-        os.sched_setaffinity(0, set(pin))
-    except OSError:
-        pass
+    # one thread per core, spread over the NUMA nodes; every thread works on its own copy of its
+    # records, first touched by itself (so it lives on the thread's node)
+    pin, pin_nodes = pick_cpus(threads)
     if wl.batch.desc is None:
         L = wl.batch.length
         m = min(wl.n, max(1, CPU_SAMPLE_BYTES // L))
@@ -333,47 +355,66 @@ def cpu_baseline(E, wl, seconds: float):
         span = int(d["len"].astype(np.uint64).sum())
     dev_tx = wl.tx[:end].cpu().numpy()
     dev_st = wl.status[:m].cpu().numpy()
-    tx = dev_tx.copy()
-    rx = wl.rx[:end].cpu().numpy().copy()
+    dev_rx = wl.rx[:end].cpu().numpy()
     caps = (0, 0, 0, 0, 0)
     build = oracle.use_native()
+    bounds = [S.shard_range(m, t, threads) for t in range(threads)]
+
+    def records_of(lo, hi):
+        """(tx, rx, desc) copies of records [lo, hi), made by the calling thread."""
+        if hi == lo:
+            return None
+        if desc is None:
+            a, b, d = lo * stride, (hi - 1) * stride + L, None
+        else:
+            a = int(desc["offset"][lo])
+            b = int(desc["offset"][hi - 1]) + int(desc["len"][hi - 1])
+            d = desc[lo:hi].copy()
+            d["offset"] -= np.uint64(a)
+        return dev_tx[a:b].copy(), dev_rx[a:b].copy(), d, hi - lo, a
+
+    def one_pass(part):  # emit tx + verify rx over one thread's records
+        if part is None:
+            return np.zeros(0, np.uint8)
+        tx, rx, d, k, _ = part
+        oracle.batch_emit(tx, d, k, stride, L, wl.kind, caps)
+        return oracle.batch_verify(rx, d, k, stride, L, wl.kind, caps)
+
+    def timed_passes(run_once, budget):
+        run_once()  # warm
+        times, t0 = [], time.perf_counter()
+        out = None
+        while len(times) < 10 or (time.perf_counter() - t0 < budget and len(times) < 200):
+            a = time.perf_counter()
+            out = run_once()
+            times.append(time.perf_counter() - a)
+        med, best = float(np.median(times)), float(min(times))
+        p10, p90 = (float(x) for x in np.percentile(times, [10, 90]))
+        return out, {"GiB/s": 2 * span / med / GIB, "best_GiB/s": 2 * span / best / GIB, "reps": len(times),
+                     "median_s": med, "spread": float((max(times) - min(times)) / med),
+                     "p10_p50_p90_GiB/s": [round(2 * span / x / GIB, 2) for x in (p90, med, p10)],
+                     "spread_p10_p90": float((p90 - p10) / med)}
+
     res = {}
-    st = None
-    # every worker thread pinned to its own CPU (pick_cpus), so the scheduler does not migrate the
-    # threads between passes
-    slot = iter(range(threads))
-    import threading
-    lock = threading.Lock()
-
-    def pin_worker():
-        with lock:
-            i = next(slot)
-        try:
-            os.sched_setaffinity(0, {pin[i]})  # Linux: pid 0 = the calling thread
-        except OSError:
-            pass
-
-    with cf.ThreadPoolExecutor(threads, initializer=pin_worker) as pool:
-        list(pool.map(lambda _: time.sleep(0.05), range(threads)))  # start (and pin) every worker
-        for t in sorted({1, threads}):
-            _oracle_pass(oracle, tx, rx, desc, m, stride, L, wl.kind, caps, t, pool)  # warm
-            times, t0 = [], time.perf_counter()
-            while len(times) < 10 or (time.perf_counter() - t0 < seconds / 2 and len(times) < 200):
-                a = time.perf_counter()
-                st = _oracle_pass(oracle, tx, rx, desc, m, stride, L, wl.kind, caps, t, pool)
-                times.append(time.perf_counter() - a)
-            med, best = float(np.median(times)), float(min(times))
-            p10, p90 = (float(x) for x in np.percentile(times, [10, 90]))
-            res[t] = {"GiB/s": 2 * span / med / GIB, "best_GiB/s": 2 * span / best / GIB, "reps": len(times),
-                      "median_s": med, "spread": float((max(times) - min(times)) / med),
-                      "p10_p50_p90_GiB/s": [round(2 * span / x / GIB, 2) for x in (p90, med, p10)],
-                      "spread_p10_p90": float((p90 - p10) / med)}
-    torch.cuda.synchronize()
+    team = PinnedTeam(pin)
     try:
-        os.sched_setaffinity(0, main_aff)
-    except OSError:
-        pass
-    parity = {"records": m, "emit_bitexact": bool(np.array_equal(tx, dev_tx)),
+        # all threads, each over its own records
+        parts = team.run(lambda i: records_of(*bounds[i]))
+        sts, res[threads] = timed_passes(lambda: team.run(lambda i: one_pass(parts[i])), seconds / 2)
+        # one thread over the whole sample (thread 0's copy)
+        if threads > 1:
+            whole = team.run(lambda i: records_of(0, m) if i == 0 else None)[0]
+            st1, res[1] = timed_passes(lambda: team.run(lambda i: one_pass(whole) if i == 0 else None)[0], seconds / 2)
+            del whole
+        else:
+            res[1] = res[threads]
+    finally:
+        team.close()
+    torch.cuda.synchronize()
+    st = np.concatenate(sts)
+    emit_ok = all(p is None or np.array_equal(p[0], dev_tx[p[4]:p[4] + p[0].size]) for p in parts)
+    tx = None
+    parity = {"records": m, "emit_bitexact": bool(emit_ok),
               "verify_bitexact": bool(np.array_equal(st, dev_st)),
               "checker": "oracle/csum_oracle.c on the cpu_baseline sample"}
     r = res[threads]
@@ -384,12 +425,14 @@ def cpu_baseline(E, wl, seconds: float):
            "spread_p10_p90": round(r["spread_p10_p90"], 3),
            "pass_rate_p10_p50_p90": r["p10_p50_p90_GiB/s"],
            "single_core_pass_rate_p10_p50_p90": res[1]["p10_p50_p90_GiB/s"],
-           "pinned_cpus": pin, "numa_node": node,
+           "pinned_cpus": pin, "numa_nodes": sorted(set(pin_nodes)),
            "host": share,
            "sample": f"{m} records of the same workload ({end / 1e9:.2f} GB per buffer, > host LLC): emit tx + "
                      f"verify rx; median of {r['reps']} passes on {threads} threads ({res[1]['reps']} on 1; the "
                      f"host is shared: the fastest pass is beside it); "
-                     f"oracle/csum_oracle.c built {build}; records split evenly over the threads"}
+                     f"oracle/csum_oracle.c built {build}; records split evenly over the threads, one thread "
+                     f"per core spread over the NUMA nodes, each on its own first-touched copy of its records "
+                     f"(the 1-thread value: one thread over the whole sample)"}
     return out, parity
 
 

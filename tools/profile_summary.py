@@ -101,10 +101,10 @@ def main():
             cfg[role]["kernel_trace_calls"] = avg_ns[role][2]
     doc[a.config] = cfg
     doc["method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                     "`python3 bench.py --config <cfg> --steps 5 --warmup 1 --cpu-seconds 0`; counters in KB "
+                     "`python3 bench.py --config <cfg> --steps 5 --warmup 1 --ramp-ms 0 --cpu-seconds 0`; counters in KB "
                      "(x1024); FETCH_SIZE doubled per MI355X_MICROARCH.md (HBM / rocprofv3: gfx950 counts half "
                      "of a 16-B/lane streaming read); mean over dispatches. kernel_trace_avg_ns from "
-                     "`rocprofv3 --kernel-trace --stats` of `bench.py --config <cfg> --steps 20`.")
+                     "`rocprofv3 --kernel-trace --stats` of `bench.py --config <cfg> --steps 20 --warmup 5` (clock ramp included).")
     with open(path, "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps({a.config: cfg}, indent=1))
