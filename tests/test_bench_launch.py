@@ -92,3 +92,26 @@ def test_bench_gpu_contract():
     n64 = d["config"]["records_per_gpu"] // 64  # 1/64 single-bit flips (a few the gates cannot see)
     assert d["ramp"]["steps"] >= 8 and n64 - 16 <= d["verify_rejected"] <= n64
     assert d["cpu_baseline"] is None  # --cpu-seconds 0
+
+
+def test_cpu_baseline_team_pinning():
+    """The CPU baseline's threads: distinct CPUs of this process's affinity set, one per core
+    first, spread over the NUMA nodes; each team thread runs pinned to its own CPU."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    aff = os.sched_getaffinity(0)
+    n = min(4, len(aff))
+    cpus, nodes = bench.pick_cpus(n)
+    assert len(cpus) == n == len(nodes) and len(set(cpus)) == n and set(cpus) <= aff
+    team = bench.PinnedTeam(cpus)
+    try:
+        got = team.run(lambda i: (i, sorted(os.sched_getaffinity(0))))
+        assert [g[0] for g in got] == list(range(n))
+        assert all(g[1] == [cpus[g[0]]] for g in got)
+        with pytest.raises(ZeroDivisionError):
+            team.run(lambda i: 1 // (i - 1))  # an exception in one thread reaches the caller
+        assert team.run(lambda i: i * i) == [i * i for i in range(n)]
+    finally:
+        team.close()
+    assert os.sched_getaffinity(0) == aff  # the caller's own mask is untouched
