@@ -9,12 +9,18 @@
 //   emit:   H2D(frames) -> smol_csum_batch_emit   -> D2H(frames)       (TxToken::consume)
 //   verify: H2D(frames) -> smol_csum_batch_verify -> D2H(status bytes) (before an RxToken)
 //
+// Frames a raw socket produced are marked with mark_raw(): their L4 bytes are the user's
+// (src/iface/packet.rs:132-136, src/socket/raw.rs:406-423), so a chunk holding one goes to the
+// device with a descriptor array whose flags carry SMOL_REC_IPHDR_ONLY for those slots (the IPv4
+// header is emitted, the L4 bytes are left alone); other chunks stay fixed-stride batches.
+//
 // Header-only; needs the HIP runtime (hip/hip_runtime_api.h, -lamdhip64) and libsmolcsum.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <cstring>
 #include <string>
 
 #include "smoltcp_checksum.hpp"
@@ -35,9 +41,15 @@ public:
                   "hipHostMalloc(ring)");
         hip_check(hipHostMalloc(reinterpret_cast<void**>(&status_), slots_, hipHostMallocDefault),
                   "hipHostMalloc(status)");
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&raw_), slots_, hipHostMallocDefault), "hipHostMalloc(raw)");
+        std::memset(raw_, 0, slots_);
         for (int k = 0; k < 2; ++k) {
             hip_check(hipMalloc(&dbuf_[k], size_t(chunk_) * slot_), "hipMalloc(chunk)");
             hip_check(hipMalloc(&dst_[k], chunk_), "hipMalloc(status)");
+            hip_check(hipMalloc(reinterpret_cast<void**>(&ddesc_[k]), size_t(chunk_) * sizeof(smol_csum_desc_t)),
+                      "hipMalloc(desc)");
+            hip_check(hipHostMalloc(reinterpret_cast<void**>(&hdesc_[k]), size_t(chunk_) * sizeof(smol_csum_desc_t),
+                                    hipHostMallocDefault), "hipHostMalloc(desc)");
         }
         for (auto& s : s_) hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
     }
@@ -46,9 +58,12 @@ public:
         for (int k = 0; k < 2; ++k) {
             (void)hipFree(dbuf_[k]);
             (void)hipFree(dst_[k]);
+            (void)hipFree(ddesc_[k]);
+            (void)hipHostFree(hdesc_[k]);
         }
         (void)hipHostFree(host_);
         (void)hipHostFree(status_);
+        (void)hipHostFree(raw_);
     }
     OffloadRing(const OffloadRing&) = delete;
     OffloadRing& operator=(const OffloadRing&) = delete;
@@ -57,6 +72,12 @@ public:
     const uint8_t* status() const { return status_; }
     uint32_t slots() const { return slots_; }
     uint32_t slot_bytes() const { return slot_; }
+
+    // Slot i holds a raw socket's frame (true) or a frame the stack built (false, the default).
+    void mark_raw(uint32_t i, bool raw = true) {
+        if (i >= slots_) throw Error(SMOL_ERANGE, "slot out of range");
+        raw_[i] = raw ? 1 : 0;
+    }
 
     // Fill the checksums of frames [0, n) in place (caps: the stack's, default Checksum::Both).
     void emit(uint32_t n, const smoltcp::phy::ChecksumCapabilities& caps = {}) { run(n, true, caps); }
@@ -76,9 +97,19 @@ private:
             const size_t bytes = size_t(m) * slot_;
             if (c >= 2) hip_check(hipStreamWaitEvent(s_[0], ev[2][k], 0), "wait d2h");  // chunk buffer free
             hip_check(hipMemcpyAsync(dbuf_[k], slot(lo), bytes, hipMemcpyHostToDevice, s_[0]), "H2D");
+            bool any_raw = false;
+            for (uint32_t j = 0; j < m && !any_raw; ++j) any_raw = raw_[lo + j] != 0;
+            if (any_raw) {  // the chunk's descriptors, raw slots flagged (hdesc_[k] is free: c-2 finished)
+                if (c >= 2) hip_check(hipEventSynchronize(ev[0][k]), "wait desc buffer");
+                for (uint32_t j = 0; j < m; ++j)
+                    hdesc_[k][j] = smol_csum_desc_t{uint64_t(j) * slot_, slot_, uint8_t(medium_),
+                                                    uint8_t(raw_[lo + j] ? SMOL_REC_IPHDR_ONLY : 0u), 0};
+                hip_check(hipMemcpyAsync(ddesc_[k], hdesc_[k], size_t(m) * sizeof(smol_csum_desc_t),
+                                         hipMemcpyHostToDevice, s_[0]), "H2D(desc)");
+            }
             hip_check(hipEventRecord(ev[0][k], s_[0]), "record");
             hip_check(hipStreamWaitEvent(s_[1], ev[0][k], 0), "wait h2d");
-            Batch b = Batch::fixed(m, slot_, slot_, medium_);
+            Batch b = any_raw ? Batch::described(ddesc_[k], m) : Batch::fixed(m, slot_, slot_, medium_);
             if (emit) eng_.emit(dbuf_[k], b, caps, nullptr, s_[1]);
             else eng_.verify(dbuf_[k], b, dst_[k], caps, s_[1]);
             hip_check(hipEventRecord(ev[1][k], s_[1]), "record");
@@ -97,8 +128,11 @@ private:
     Medium medium_;
     uint8_t* host_ = nullptr;
     uint8_t* status_ = nullptr;
+    uint8_t* raw_ = nullptr;  // per slot: a raw socket's frame
     uint8_t* dbuf_[2] = {nullptr, nullptr};
     uint8_t* dst_[2] = {nullptr, nullptr};
+    smol_csum_desc_t* ddesc_[2] = {nullptr, nullptr};
+    smol_csum_desc_t* hdesc_[2] = {nullptr, nullptr};
     hipStream_t s_[3] = {};
 };
 

@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "../../smoltcp_amd/host/offload_ring.hpp"
 #include "../../smoltcp_amd/host/smoltcp_checksum.hpp"
 
 namespace ck = smoltcp::wire::checksum;
@@ -226,6 +227,53 @@ static int run_offload(uint32_t n) {
     return 0;
 }
 
+// Raw-socket frames through OffloadRing (SMOL_REC_IPHDR_ONLY): every 5th slot
+// carries a frame whose L4 checksum the user wrote (0xBEEF, wrong on purpose), marked raw.  After
+// emit, raw frames keep their L4 bytes and get a valid IPv4 header; the others pass the host gates.
+// Verify then accepts the raw frames on their IPv4 gate alone (status UNSUPPORTED: no L4 checksum
+// on their path) and checks the others fully.  Chunks of 1000 slots: some hold no raw frame
+// (fixed-stride batches), the others go through descriptors.
+static int run_raw(uint32_t n) {
+    const uint32_t stride = 1536;
+    smoltcp_amd::OffloadRing ring(0, n, stride, smoltcp_amd::Medium::Ip, 1000);
+    std::vector<std::vector<uint8_t>> want(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        auto f = frame(i, stride);
+        const bool raw = i % 5 == 0 && (i / 1000) % 3 != 1;  // chunk 1, 4, ...: no raw frame
+        if (raw) {
+            const uint32_t fo = f[9] == 17 ? 26 : 36;
+            f[fo] = 0xBE, f[fo + 1] = 0xEF;
+        }
+        std::fill(ring.slot(i), ring.slot(i) + stride, 0);
+        std::copy(f.begin(), f.end(), ring.slot(i));
+        ring.mark_raw(i, raw);
+        want[i] = f;
+    }
+    ring.emit(n);
+    uint32_t bad = 0, raws = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* b = ring.slot(i);
+        if (i % 5 == 0 && (i / 1000) % 3 != 1) {
+            ++raws;
+            const bool l4_same = std::equal(want[i].begin() + 20, want[i].end(), b + 20);
+            bad += !(l4_same && ck::data({b, 20}) == 0xffff);
+        } else {
+            bad += !host_accepts(b);
+        }
+    }
+    EXPECT(bad == 0, "%u frames wrong after emit", bad);
+    ring.verify(n);
+    uint32_t vbad = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t st = ring.status()[i];
+        if (i % 5 == 0 && (i / 1000) % 3 != 1) vbad += !(smoltcp_amd::accepted(st) && (st & SMOL_ST_UNSUPPORTED));
+        else vbad += smoltcp_amd::accepted(st) != host_accepts(ring.slot(i));
+    }
+    EXPECT(vbad == 0, "%u verify statuses wrong", vbad);
+    std::printf("raw %u frames (%u raw): emit kept the user's L4 bytes, verify gated their IPv4 header only\n", n, raws);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) return 2;
     std::string mode = argv[1];
@@ -234,6 +282,7 @@ int main(int argc, char** argv) {
         if (mode == "vectors" && argc > 2) rc = run_vectors(argv[2]);
         else if (mode == "nodev") rc = run_nodev();
         else if (mode == "offload") rc = run_offload(argc > 2 ? uint32_t(std::atoi(argv[2])) : 10000);
+        else if (mode == "raw") rc = run_raw(argc > 2 ? uint32_t(std::atoi(argv[2])) : 10000);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 1;

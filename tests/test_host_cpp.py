@@ -74,6 +74,16 @@ def test_cpp_offload_device_roundtrip(binary):
 
 
 @pytest.mark.gpu
+def test_cpp_offload_ring_raw_frames(binary):
+    """OffloadRing with raw-socket slots (SMOL_REC_IPHDR_ONLY through per-chunk descriptors):
+    the user's L4 bytes survive emit, verify gates their IPv4 header only."""
+    assert _has_gpu()
+    r = subprocess.run([binary, "raw", "7003"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "kept the user's L4 bytes" in r.stdout
+
+
+@pytest.mark.gpu
 def test_loopback_ring_c1_analogue():
     """tools/loopback_ring (OffloadRing: pinned ring -> HBM -> emit / verify -> host): every
     emitted frame passes both the GPU verify and the host scalar gates."""
