@@ -231,6 +231,26 @@ def _cpulist(text: str):
     return out
 
 
+def cgroup_cpu_stat() -> dict:
+    """The cgroup's CPU accounting (cgroup v2 cpu.stat): usage and CFS bandwidth throttling. A job
+    whose threads exceed its CPU quota within a period is stopped until the next one; the CPU
+    baseline reports how often that happened while it ran."""
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                    out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def cgroup_delta(a: dict, b: dict) -> dict:
+    return {k: b[k] - a[k] for k in b if k in a}
+
+
 def pick_cpus(threads: int):
     """`threads` CPUs of this process's affinity set for the CPU baseline: one hardware thread per
     core (SMT siblings only once every core has one), taken round-robin over the NUMA nodes so that
@@ -395,16 +415,20 @@ def cpu_baseline(E, wl, seconds: float):
                      "p10_p50_p90_GiB/s": [round(2 * span / x / GIB, 2) for x in (p90, med, p10)],
                      "spread_p10_p90": float((p90 - p10) / med)}
 
-    res = {}
+    res, cg = {}, {}
     team = PinnedTeam(pin)
     try:
         # all threads, each over its own records
         parts = team.run(lambda i: records_of(*bounds[i]))
+        c0 = cgroup_cpu_stat()
         sts, res[threads] = timed_passes(lambda: team.run(lambda i: one_pass(parts[i])), seconds / 2)
+        cg[threads] = cgroup_delta(c0, cgroup_cpu_stat())
         # one thread over the whole sample (thread 0's copy)
         if threads > 1:
             whole = team.run(lambda i: records_of(0, m) if i == 0 else None)[0]
+            c0 = cgroup_cpu_stat()
             st1, res[1] = timed_passes(lambda: team.run(lambda i: one_pass(whole) if i == 0 else None)[0], seconds / 2)
+            cg[1] = cgroup_delta(c0, cgroup_cpu_stat())
             del whole
         else:
             res[1] = res[threads]
@@ -427,6 +451,9 @@ def cpu_baseline(E, wl, seconds: float):
            "single_core_pass_rate_p10_p50_p90": res[1]["p10_p50_p90_GiB/s"],
            "pinned_cpus": pin, "numa_nodes": sorted(set(pin_nodes)),
            "host": share,
+           "cgroup_cpu_stat_delta": {"all_threads": cg.get(threads, {}), "one_thread": cg.get(1, {}),
+                                     "what": "cgroup v2 cpu.stat over the timed passes: CPU time used and "
+                                             "CFS quota throttling (periods the job was stopped)"},
            "sample": f"{m} records of the same workload ({end / 1e9:.2f} GB per buffer, > host LLC): emit tx + "
                      f"verify rx; median of {r['reps']} passes on {threads} threads ({res[1]['reps']} on 1; the "
                      f"host is shared: the fastest pass is beside it); "
