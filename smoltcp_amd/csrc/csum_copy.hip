@@ -68,8 +68,8 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 
 }  // namespace copy2
 
-template <int G, int U, bool IMPLICIT, int UW0, int UB, bool OWN>
-__device__ __forceinline__ void copy_body(const KParams& p) {
+template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0>
+__global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
     constexpr int GPB = 256 / G;
     // slots per lane loaded before the parse (UW0, or enough for the window plus 8 chunks past it):
@@ -79,13 +79,6 @@ __device__ __forceinline__ void copy_body(const KParams& p) {
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     __shared__ u32x4 win[GPB][WIN_CH];
     __shared__ Geom geo[GPB];
-    // OWN: the 128-B line that holds record r+1's first byte is written whole by r+1's group when
-    // r+1's group is the next group of the same wavefront (tl: record r's chunks in that line,
-    // hnd: whether r hands them over; na0 / nlen: each group's record start and length)
-    constexpr int GPW = 64 / G;
-    __shared__ u32x4 tl[OWN ? GPB : 1][8];
-    __shared__ uint32_t hnd[OWN ? GPB : 1], nlen[OWN ? GPB : 1];
-    __shared__ uint64_t na0[OWN ? GPB : 1];
 
     const int lane = (int)(threadIdx.x % G);
     const int gib = (int)(threadIdx.x / G);
@@ -96,13 +89,6 @@ __device__ __forceinline__ void copy_body(const KParams& p) {
 
     for (uint64_t r = (uint64_t)blockIdx.x * GPB + gib; r < p.n; r += ngroups) {
         const RecRef rr = rec_at<IMPLICIT, true>(p, r);
-        if constexpr (OWN) {
-            if (lane == 0) {
-                na0[gib] = rr.a0;
-                nlen[gib] = (rr.kind & KIND_BAD_COPY) ? 0u : rr.len;
-                hnd[gib] = 0u;
-            }
-        }
         if (rr.kind & KIND_BAD_COPY) {  // the copy range does not fit: record left untouched
             if (lane == 0 && p.status) ((gu8)p.status)[r] = (uint8_t)SMOL_ST_MALFORMED;
             continue;
@@ -249,31 +235,6 @@ __device__ __forceinline__ void copy_body(const KParams& p) {
         }
         const bool far = f0b != NOF || f1b != NOF || f2b != NOF;
         const int len = (int)rr.len;
-        // OWN: hand this record's chunks in the next record's first line to the next group when
-        // the next record starts right where this one ends, both are long enough for that line
-        // to hold nothing else and no field of this record lies in it
-        uint32_t kt = ~0u;  // first chunk handed over (~0: none)
-        if constexpr (OWN) {
-            bool hand = false;
-            if ((gib % GPW) != GPW - 1 && r + 1 < p.n) {
-                const uint64_t a1 = na0[gib + 1];
-                const uint32_t l1 = nlen[gib + 1];
-                const uint64_t L0n = a1 & ~127ull;
-                const uint32_t fip = g.fam == 4 ? g.ip_off + 10 : NO_FIELD;
-                const uint32_t fl4 = l4 ? g.l4_off + g.fo : NO_FIELD;
-                const uint32_t fin = g.in_off ? g.in_off + 10 : NO_FIELD;
-                auto clear = [&](uint32_t f) { return f == NO_FIELD || rr.a0 + f + 2 <= L0n; };
-                hand = l1 > 0 && rr.a0 + rr.len == a1 && rr.len >= 256 && (uint64_t)l1 + a1 >= L0n + 128 &&
-                       clear(fip) && clear(fl4) && clear(fin);
-                if (hand) kt = (uint32_t)((L0n - base) >> 4);
-            }
-            if (lane == 0) hnd[gib] = hand ? 1u : 0u;
-        }
-        // LDS slot of chunk k when it is handed over, else -1
-        auto tail_slot = [&](uint32_t k) -> int {
-            if constexpr (!OWN) return -1;
-            return k >= kt ? (int)(k - kt) : -1;
-        };
 
         // ---- sum round 1; store its chunks past the window ----
         uint32_t acc = 0;
@@ -286,11 +247,7 @@ __device__ __forceinline__ void copy_body(const KParams& p) {
             if (in) {
                 const int pos = (int)(16u * k) - (int)head;
                 acc = sum_chunk(gm[u], pos, s1, acc);
-                if (!w) {
-                    const int t = tail_slot(k);
-                    if (t >= 0) tl[gib][t] = gm[u];
-                    else store_part((gu8)base + 16u * k, gm[u], -pos, len - pos, f0b - pos, f1b - pos, f2b - pos);
-                }
+                if (!w) store_part((gu8)base + 16u * k, gm[u], -pos, len - pos, f0b - pos, f1b - pos, f2b - pos);
             }
         }
         // generic chunks beyond round 1 (a copy range that starts or ends far from the record's edges)
@@ -304,9 +261,7 @@ __device__ __forceinline__ void copy_body(const KParams& p) {
             if (in) {
                 const int pos = (int)(16u * k) - (int)head;
                 acc = sum_chunk(m, pos, s1, acc);
-                const int t = tail_slot(k);
-                if (t >= 0) tl[gib][t] = m;
-                else store_part((gu8)base + 16u * k, m, -pos, len - pos, f0b - pos, f1b - pos, f2b - pos);
+                store_part((gu8)base + 16u * k, m, -pos, len - pos, f0b - pos, f1b - pos, f2b - pos);
             }
         }
 
@@ -321,9 +276,7 @@ __device__ __forceinline__ void copy_body(const KParams& p) {
             const int pos = (int)(16u * k) - (int)head;
             acc = sum_chunk(m, pos, s1, acc);
             const gu8 dst = (gu8)base + 16u * k;
-            const int t = tail_slot(k);
-            if (t >= 0) tl[gib][t] = m;
-            else if (!far) *(GMEM u32x4*)dst = m;
+            if (!far) *(GMEM u32x4*)dst = m;
             else store_part(dst, m, 0, 16, f0b - pos, f1b - pos, f2b - pos);
         };
         if constexpr (UB > 0) {
@@ -346,60 +299,20 @@ __device__ __forceinline__ void copy_body(const KParams& p) {
         finish_gates<G, MODE_COPY, false, decltype(rd), WIN>(p, g, acc, rd, winb, head, rr.a0, r, lane,
                                                               reinterpret_cast<uint8_t*>(wn));
         wave_lds_sync();
-        uint32_t kw = 0;
-        if constexpr (OWN) {
-            // the previous group handed its chunks of this record's first line over: that line
-            // goes out whole, its bytes before the record from them, the rest from the window
-            if ((gib % GPW) != 0 && hnd[gib - 1]) {
-                const uint64_t L0 = rr.a0 & ~127ull;
-                if (lane < 8) {
-                    const uint64_t a = L0 + 16ull * (uint32_t)lane;
-                    u32x4 c;
-                    if (a < base) {
-                        c = tl[gib - 1][lane];
-                    } else {
-                        c = wn[(a - base) >> 4];
-                        if (a == base && head) {
-                            const u32x4 t = tl[gib - 1][lane];
-                            const uint32_t m0 = byte_mask(0, (int)head, 0), m1 = byte_mask(0, (int)head, 1);
-                            const uint32_t m2 = byte_mask(0, (int)head, 2), m3 = byte_mask(0, (int)head, 3);
-                            c.x = (t.x & m0) | (c.x & ~m0);
-                            c.y = (t.y & m1) | (c.y & ~m1);
-                            c.z = (t.z & m2) | (c.z & ~m2);
-                            c.w = (t.w & m3) | (c.w & ~m3);
-                        }
-                    }
-                    *(GMEM u32x4*)a = c;
-                }
-                kw = (uint32_t)((L0 + 128 - base) >> 4);
-            }
-        }
-        for (uint32_t k = kw + (uint32_t)lane; k < (uint32_t)WIN_CH && k < nch; k += G) {
+        for (uint32_t k = (uint32_t)lane; k < (uint32_t)WIN_CH && k < nch; k += G) {
             const int pos = (int)(16u * k) - (int)head;
             store_part((gu8)base + 16u * k, wn[k], -pos, len - pos, NOF, NOF, NOF);
         }
-        wave_lds_sync();  // the window (and OWN's hand-over) is rewritten by the group's next record
+        wave_lds_sync();  // the window is rewritten by the group's next record
     }
 }
 
-template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0>
-__global__ __launch_bounds__(256) void copy_kernel(KParams p) {
-    copy_body<G, U, IMPLICIT, UW0, UB, false>(p);
-}
-
-// OWN (variant 18) holds one more value across the body rounds; 5 waves per SIMD are kept
-template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void copy_own_kernel(KParams p) {
-    copy_body<G, U, IMPLICIT, UW0, UB, true>(p);
-}
-
-template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0, bool OWN = false>
+template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0>
 hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    if constexpr (OWN) hipLaunchKernelGGL((copy_own_kernel<G, U, IMPLICIT, UW, UB>), dim3(blocks), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB>), dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -429,21 +342,6 @@ hipError_t launch_copy2(int shape, const KParams& p, uint32_t max_blocks, hipStr
 
 hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     return p.desc == nullptr ? launch_copy2<true>(shape, p, max_blocks, s) : launch_copy2<false>(shape, p, max_blocks, s);
-}
-
-// Variant 18: copy_kernel with whole-line hand-over between neighbouring groups (OWN).
-template <bool IMPLICIT>
-hipError_t launch_copy_own(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    switch (shape) {
-        case CFG_G8U7: return launch_copy2_one<IMPLICIT, 8, 4, 4, 0, true>(p, max_blocks, s);
-        case CFG_G16U6: return launch_copy2_one<IMPLICIT, 16, 5, 1, 1, true>(p, max_blocks, s);
-        case CFG_G32U4: return launch_copy2_one<IMPLICIT, 32, 2, 1, 0, true>(p, max_blocks, s);
-        default: return launch_copy2_one<IMPLICIT, 16, 4, 1, 2, true>(p, max_blocks, s);  // CFG_G16U4
-    }
-}
-
-hipError_t launch_copy_v18(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    return p.desc == nullptr ? launch_copy_own<true>(shape, p, max_blocks, s) : launch_copy_own<false>(shape, p, max_blocks, s);
 }
 
 }  // namespace smolcsum
