@@ -487,7 +487,7 @@ def gather_floats(vals, device=None):
     import torch
     import torch.distributed as dist
 
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [list(vals)]
     t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
@@ -549,7 +549,11 @@ def main(argv=None):
         return 2
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if world > 1:
+    # one process group per job over RCCL, for the barriers and the max-over-ranks reduction only
+    # (no collective on the data path); under a launcher (WORLD_SIZE set) also at world size 1, so
+    # that a one-GPU box runs the same RCCL calls as the 8-GPU node
+    pg = world > 1 or "WORLD_SIZE" in os.environ
+    if pg:
         dist.init_process_group("nccl", device_id=dev)
 
     eng = E.ChecksumEngine(local)
@@ -592,7 +596,7 @@ def main(argv=None):
 
     # The timed region: K steps with nothing between the kernels (timing events at the kernel
     # boundaries cost ~2 % of a step, tools/exp_timing.py).
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -600,7 +604,7 @@ def main(argv=None):
         step()
     torch.cuda.synchronize()
     mine = time.perf_counter() - t0
-    if world > 1:
+    if pg:
         dist.barrier()
     elapsed = S.max_over_ranks(mine, device=dev)
 
@@ -707,7 +711,8 @@ def main(argv=None):
             "dtype": "u8",
             "data": "synthetic: device-generated packets (splitmix64 payload, seeded), HBM-resident",
             "config": {"workload": wl.workload, "records_per_gpu": wl.n, "parallelism": f"shard x{world} (no collective)",
-                       "checksummed_bytes_per_step_per_gpu": 2 * wl.span_bytes},
+                       "checksummed_bytes_per_step_per_gpu": 2 * wl.span_bytes,
+                       "process_group": dist.get_backend() if pg else None},
             "roofline": {"bound": "hbm", "kernel": f"{eng.kernel_name(dop, wl.desc_bytes > 0)} ({dop})", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": tsrc,
@@ -735,7 +740,7 @@ def main(argv=None):
         if unfused:
             out["unfused_tx"] = unfused
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg:
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -94,6 +94,28 @@ def test_bench_gpu_contract():
     assert d["cpu_baseline"] is None  # --cpu-seconds 0
 
 
+@pytest.mark.gpu
+def test_bench_under_torchrun_rccl():
+    """The driver's N > 1 launch (torch.distributed.run, one rank per GPU) at the size a one-GPU
+    box allows: one rank, with the RCCL process group, barriers, max-over-ranks all_reduce and
+    per-rank all_gather that every rank of the 8-GPU run makes."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "1", "--config", "c2",
+           "--steps", "3", "--warmup", "1", "--cpu-seconds", "0", "--ramp-ms", "50"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 1 and d["config"]["process_group"] == "nccl"
+    assert [p["rank"] for p in d["per_rank"]] == [0] and d["value"] > 0
+
+
 def test_cpu_baseline_team_pinning():
     """The CPU baseline's threads: distinct CPUs of this process's affinity set, one per core
     first, spread over the NUMA nodes; each team thread runs pinned to its own CPU."""
