@@ -9,3 +9,5 @@ timeout -k 10 600 python -u -m pytest tests/test_bench_launch.py -m gpu -x -v --
 tail -4 $O/tests.log
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_c2.log 2>&1 || { tail -20 $O/bench_c2.log; exit 1; }
 tail -1 $O/bench_c2.log | cut -c1-400
+timeout -k 10 300 python tools/exp_tail.py > $O/tail.log 2>&1 || { tail -20 $O/tail.log; exit 1; }
+grep round $O/tail.log
