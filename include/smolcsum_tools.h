@@ -39,7 +39,7 @@ int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
 /* Kernel variant (-1 = automatic: 7 for emit over descriptor batches, 13 for verify over
- * descriptor batches, 5 otherwise; 17 for copy-emit).  The
+ * descriptor batches, 19 for fixed-stride emit, 5 otherwise; 17 for copy-emit).  The
  * "walk" kernel (a group parses and finishes its own record) reads 16-byte chunks on a grid that
  * starts at the record's 16-byte boundary: 0 = non-temporal loads + register prefetch of the next
  * step, 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch; or at its
@@ -50,7 +50,9 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
  * 16-byte grid with plain loads and no prefetch.  9 / 10 = variant 5 with the first two / the first
  * 16-byte chunk of every lane's step loaded cached, so that the lines holding the fields are
  * resident in L2 when emit stores them (fixed-stride emit only; elsewhere 5).  13 = variant 5
- * without the prefetch.  Copy-emit: 1 / 8 / 11 / 16 = the walk kernel in its copy mode (prefetch /
+ * without the prefetch.  19 = variant 5 whose emit writes the 64-byte segments holding an IPv4
+ * record's fields whole where no neighbouring record's field shares them (the default for
+ * fixed-stride emit; elsewhere 5).  Copy-emit: 1 / 8 / 11 / 16 = the walk kernel in its copy mode (prefetch /
  * two aligned source chunks / one chunk + the next lane's / dword-aligned source + one dword from
  * the next lane); 17 (default) = copy_kernel (csum_copy.hip), whose shapes are 16 x 4 with 32 body
  * chunks in round 1 (default, shape 8), 16 x 3 (1), 8 x 6 (0), 8 x 4 (7), 16 x 5 (2), 16 x 4 with

@@ -60,13 +60,14 @@ namespace smolcsum {
 // the record written (WHOLE, see walk_step).  Measured variants that lost are in DESIGN.md §6.
 template <int VAR>
 struct VarT {
-    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13;
+    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19;
     static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16;
-    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13;
+    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19;
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
     static constexpr bool SHUF2 = VAR == 16;
+    static constexpr bool SEGW = VAR == 19;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
 };
 
 template <bool LINE>
@@ -336,11 +337,29 @@ struct Walk {
     int s1;          // end of the summed span, relative to the record start
     uint32_t acc, acc2;
     uint32_t fip, fl4, fin;  // MODE_COPY: record offsets of the fields emit writes (NO_FIELD if none)
+    int32_t segA, segB;      // SEGW: record-relative starts of the 64-B segments written whole (SEG_NONE: none)
     bool far;                // MODE_COPY, WHOLE: a field lies (partly) past the LDS window
 };
 
 constexpr uint32_t NO_FIELD = 0x3fffffffu;
+constexpr int32_t SEG_NONE = -(1 << 30);
 constexpr uint32_t MF_NONE = 0x3fffu;  // no field (finish_gates)
+
+// SEGW (fixed-stride emit): the record a group is on (tag = low 32 bits of its index) and the
+// record-offset range [lo, hi) of the fields emit may write there (lo = NO_FIELD, hi = 0: none),
+// published in LDS after the parse for the neighbouring groups of the wavefront.  The tag is stored
+// twice so that each neighbour reads its pair with one 8-byte LDS load.
+struct SegInfo {
+    uint32_t tag, hi;   // read by the next group
+    uint32_t tag2, lo;  // read by the previous group
+};
+
+// The record offsets of the fields emit may write (NO_FIELD: none): a superset of finish_gates'.
+__device__ __forceinline__ void emit_fields(const Geom& g, uint32_t f[3]) {
+    f[0] = g.fam == 4 ? g.ip_off + 10 : NO_FIELD;
+    f[1] = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? g.l4_off + g.fo : NO_FIELD;
+    f[2] = g.in_off ? g.in_off + 10 : NO_FIELD;
+}
 
 // The gates of one record (MODE_EMIT / MODE_VERIFY / MODE_COPY), run by its whole group once every
 // lane holds its part `acc` of the aligned-word sum over [0, span_end): the header bytes the lanes
@@ -348,10 +367,14 @@ constexpr uint32_t MF_NONE = 0x3fffu;  // no field (finish_gates)
 // the LDS window (`winb`, record byte o at head + o), and lane 0 finishes and writes the record.
 // WINB > 0 (MODE_COPY, WHOLE): field bytes inside the first WINB bytes of the chunk grid go into the
 // LDS window (`winw`), whose chunks the caller stores afterwards, instead of to global memory.
-template <int G, int MODE, bool NHC, class RD, int WINB = 0>
+// SEGP (fixed-stride emit, SEGW): the 64-B segments wsA / wsB (~0: none) go out whole from the
+// window afterwards; a field is patched into the window, and stored to global memory unless both
+// of its bytes lie in those segments.
+template <int G, int MODE, bool NHC, class RD, int WINB = 0, bool SEGP = false>
 __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, uint32_t acc, const RD& rd,
                                              const uint8_t* winb, uint32_t head, uint64_t a0, uint64_t r,
-                                             int lane, uint8_t* winw = nullptr) {
+                                             int lane, uint8_t* winw = nullptr, uint64_t wsA = ~0ull,
+                                             uint64_t wsB = ~0ull) {
     constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
     const bool odd = (a0 & 1u) != 0;
     // Header bytes [0, l4_off) that the lanes summed (taken out of the L4 sum), the IPv4
@@ -487,7 +510,19 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
                 l4_ok = caps_rx(gate_caps) ? l4_valid : 1u;
             }
         }
-        if (EMITS && WINB > 0) {
+        if (EMITS && SEGP) {
+            auto put = [&](uint32_t f, uint32_t v) {
+                const uint64_t x0 = (a0 + f) & ~63ull, x1 = (a0 + f + 1) & ~63ull;
+                const bool cov = (x0 == wsA || x0 == wsB) && (x1 == wsA || x1 == wsB);
+                for (uint32_t i = 0; i < 2; ++i)
+                    if (head + f + i < (uint32_t)WINB) winw[head + f + i] = (uint8_t)(i ? v : v >> 8);
+                if (!cov) store_be16(wrec + f, v);
+            };
+            if (fip != MF_NONE) put(fip, vip);
+            if (fin != MF_NONE) put(fin, vin);
+            if (fl4 != MF_NONE) put(fl4, vl4);
+            if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
+        } else if (EMITS && WINB > 0) {
             auto put = [&](uint32_t f, uint32_t v) {
                 for (uint32_t i = 0; i < 2; ++i) {
                     const uint8_t b = (uint8_t)(i ? v : v >> 8);
@@ -542,10 +577,10 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
-          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false>
+          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false, bool SEGW = false>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
-                                          int gib) {
+                                          int gib, SegInfo* si = nullptr) {
     constexpr bool COPY = MODE == MODE_COPY;
     // where the record geometry lives (Walk::g / Walk::gr): registers for emit with the register
     // prefetch, LDS otherwise
@@ -694,14 +729,59 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const Geom& g = GREG ? w.gr : *w.g;
             // the lanes sum [0, span_end): the header part is subtracted at the end
             w.s1 = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? (int)g.span_end : 0;
-            if (COPY) {
-                w.fip = g.fam == 4 ? g.ip_off + 10 : NO_FIELD;
-                w.fl4 = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? g.l4_off + g.fo : NO_FIELD;
-                w.fin = g.in_off ? g.in_off + 10 : NO_FIELD;
-                auto past = [&](uint32_t f) { return f != NO_FIELD && head + f + 2 > (uint32_t)WIN; };
-                w.far = past(w.fip) || past(w.fl4) || past(w.fin);
-            }
-        }
+            if constexpr (SEGW) {
+                // publish every field finish_gates may write (a superset is safe), then decide which
+                // of this record's field segments go out whole (see the finish below)
+                uint32_t f[3], lo = NO_FIELD, hi = 0;
+                emit_fields(g, f);
+                for (int j = 0; j < 3; ++j)
+                    if (f[j] != NO_FIELD) {
+                        lo = f[j] < lo ? f[j] : lo;
+                        hi = f[j] + 2 > hi ? f[j] + 2 : hi;
+                    }
+                if (lane == 0) {
+                    SegInfo e;
+                    e.tag = e.tag2 = (uint32_t)w.r;
+                    e.lo = lo;
+                    e.hi = hi;
+                    si[gib] = e;
+                }
+                w.segA = w.segB = SEG_NONE;
+                // IPv4 records only (an IPv4 header and an L4 field: two store events per record);
+                // the neighbours' field bounds, record-relative: the previous record's end by pend,
+                // the next one's start at nbeg (another wavefront or another record: unknown)
+                if (g.fam == 4 && p.stride >= 64 && p.n < 0xFFFFFFFFull && w.cur.len < (1u << 29)) {
+                    wave_lds_sync();  // the neighbours' entries
+                    constexpr int GPW = 64 / G;
+                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                    const uint64_t r = w.r;
+                    int32_t pend = 1 << 30, nbeg = -(1 << 30);
+                    const int32_t st = (int32_t)(p.stride < (1ull << 29) ? p.stride : (1ull << 29));
+                    if ((gib % GPW) != 0) {
+                        const u32x2 q = *reinterpret_cast<const u32x2*>(&si[gib - 1].tag);
+                        if (r > 0 && q.x == (uint32_t)(r - 1)) pend = (int32_t)(q.y < (1u << 29) ? q.y : (1u << 29)) - st;
+                    }
+                    if ((gib % GPW) != GPW - 1) {
+                        const u32x2 q = *reinterpret_cast<const u32x2*>(&si[gib + 1].tag2);
+                        if (q.x == (uint32_t)(r + 1)) nbeg = st + (int32_t)(q.y < (1u << 29) ? q.y : (1u << 29));
+                    }
+                    // record-relative starts of the segments holding the first and the last field byte
+                    const int32_t ph = (int32_t)(w.cur.a0 & 63u);
+                    const int32_t rA = ((ph + (int32_t)lo) & ~63) - ph, rB = ((ph + (int32_t)hi - 1) & ~63) - ph;
+                    const int32_t len = (int32_t)w.cur.len;
+                    const bool packed = p.len == p.stride;
+                    const bool lastrec = r + 1 >= p.n;
+                    // the window holds the record's chunks only (past its last one: the dummy line)
+                    const int32_t wend = 16 * (int32_t)(w.nch < (uint32_t)WIN_CH ? w.nch : (uint32_t)WIN_CH) - (int32_t)head;
+                    auto whole = [&](int32_t rel) {
+                        return rB <= rA + 64 && rel + 64 <= wend &&
+                               (rel >= 0 || (packed && r > 0 && pend <= rel)) &&
+                               (rel + 64 <= len || (packed && !lastrec && nbeg >= rel + 64));
+                    };
+                    if (whole(rA)) w.segA = rA;
+                    if (rB != rA && whole(rB)) w.segB = rB;
+                }
+            }        }
     }
     // MODE_COPY: store the payload bytes of this step (all of them, summed or not).  WHOLE: store
     // every byte of the record instead (the bytes outside the payload unchanged), so that no cache
@@ -795,8 +875,37 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const uint32_t tot = group_sum<G>(s_rel);
             if (lane == 0) ((gu16)p.out16)[r] = (uint16_t)bswap16(fold32(tot));
         } else {
-            finish_gates<G, MODE, NHC, decltype(rd), (COPY && WHOLE) ? WIN : 0>(
-                p, GREG ? w.gr : *w.g, w.acc, rd, winb, head, w.cur.a0, r, lane, reinterpret_cast<uint8_t*>(win));
+            // SEGW: the 64-B segments that hold the fields go out whole from the LDS window, the
+            // fields patched in: a whole segment costs HBM a plain write where a 2-B store costs a
+            // read-modify-write (measured: C2 emit 0.305 -> 0.285 ms when every segment goes out
+            // whole).  A segment also holds bytes of the neighbouring records; it is written whole
+            // only when none of their fields lies in it (the field ranges their groups of this
+            // wavefront publish after the parse say so), it holds no byte outside the batch's
+            // records and the window holds all of it.  Fields outside such segments are stored as
+            // 2-B fields.
+            uint64_t wsA = ~0ull, wsB = ~0ull;
+            if constexpr (SEGW) {  // the segments decided after the parse (step 0)
+                if (w.segA != SEG_NONE) wsA = w.cur.a0 + (int64_t)w.segA;
+                if (w.segB != SEG_NONE) wsB = w.cur.a0 + (int64_t)w.segB;
+            }
+            finish_gates<G, MODE, NHC, decltype(rd), ((COPY && WHOLE) || SEGW) ? WIN : 0, SEGW>(
+                p, GREG ? w.gr : *w.g, w.acc, rd, winb, head, w.cur.a0, r, lane, reinterpret_cast<uint8_t*>(win),
+                wsA, wsB);
+            if constexpr (SEGW) {
+                if (wsA != ~0ull || wsB != ~0ull) {
+                    wave_lds_sync();
+                    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                    if (wsA != ~0ull && lane < 8) {
+                        const uint64_t d = wsA + 8u * (uint32_t)lane;
+                        *(GMEM u32x2*)d = *reinterpret_cast<const u32x2*>(winb + (d - base));
+                    }
+                    if (wsB != ~0ull && lane < 8) {
+                        const uint64_t d = wsB + 8u * (uint32_t)lane;
+                        *(GMEM u32x2*)d = *reinterpret_cast<const u32x2*>(winb + (d - base));
+                    }
+                    wave_lds_sync();  // the window is rewritten by the group's next record
+                }
+            }
             if constexpr (COPY && WHOLE) {  // the window chunks, fields patched in
                 wave_lds_sync();
                 for (uint32_t k = (uint32_t)lane; k < (uint32_t)WIN_CH && k < w.nch; k += G) {
@@ -856,10 +965,15 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "group size");
     __shared__ u32x4 win[GPB][Grid<LINE>::WIN_CH];
     __shared__ Geom geo[GPB];
+    constexpr bool SEGW = VarT<VAR>::SEGW && MODE == MODE_EMIT && IMPLICIT && LINE && !NHC;
+    __shared__ SegInfo segi[SEGW ? GPB : 1];
 
     const int lane = (int)(threadIdx.x % G);
     const int gib = (int)(threadIdx.x / G);
     const uint64_t ngroups = (uint64_t)gridDim.x * GPB;
+    if constexpr (SEGW) {
+        if (lane == 0) segi[gib].tag = segi[gib].tag2 = ~0u;  // no record yet (read by the neighbours)
+    }
     Walk w;
     w.r = (uint64_t)blockIdx.x * GPB + gib;
     if (w.r >= p.n) return;
@@ -876,6 +990,7 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     w.acc = w.acc2 = 0;
     w.fip = w.fl4 = w.fin = NO_FIELD;
     w.far = false;
+    w.segA = w.segB = SEG_NONE;
 
     Regs<U, COPY> va;
     if (PF) {
@@ -884,8 +999,8 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
                                                   shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF>(p, w, va, vb, lane, ngroups, &win[gib][0], gib)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF>(p, w, vb, va, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi)) break;
         }
     } else {
         while (true) {
@@ -932,6 +1047,7 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 5: return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
         case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
+        case 19: return launch_shape<MODE, IMPLICIT, 19>(shape, p, max_blocks, s);
         case 9:
         case 10:
             if constexpr (MODE == MODE_EMIT && IMPLICIT) {
@@ -950,7 +1066,7 @@ template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
     // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
-    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13) {
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);

@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r3f
+O=${OUT:-gpurun_out/r3f}
 mkdir -p $O
 step() {  # step <name> <seconds> <cmd...>: stop on the first failure
     local name=$1 secs=$2; shift 2
