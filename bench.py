@@ -625,7 +625,9 @@ def main(argv=None):
 
     # Emit's floor (rank 0): the read-only stream probe over the TX buffer, and the same stream plus
     # emit's scattered field stores (smol_csum_tool_field_probe: 2-B stores at the records' field
-    # offsets, one store event per field per record).  An in-place emit cannot beat the second.
+    # offsets, one store event per field per record): the floor of an emit that stores its fields as
+    # 2-B writes.  Fixed-stride emit (variant 19) writes most IPv4 field segments whole and runs
+    # under it.
     probe = floor = None
     if rank == 0 and wl.copy is None:
         sink = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -652,7 +654,9 @@ def main(argv=None):
         floor = {"kernel": "field_probe_kernel", "ms": round(fp_ms, 4), "read_only_ms": round(ro_ms, 4),
                  "what": f"the TX buffer streamed once (best read pattern) + a 2-B store at offsets {f1}"
                          + (f" and {f2}" if f2 != 0xFFFFFFFF else "") + f" of every {stride}-B record "
-                         "(emit's store events, no parse / gates): the time an in-place emit cannot beat"}
+                         "(emit's store events as 2-B writes, no parse / gates): the floor of an emit that "
+                         "stores its fields as 2-B writes; whole 64-B field segments (fixed-stride emit, "
+                         "variant 19) run under it"}
 
     unfused = None
     if wl.copy is not None and rank == 0:

@@ -75,7 +75,8 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
 /* Emit's floor probe: the stream-read probe over `bytes` plus emit's store events — a big-endian
  * 2-byte store at record offsets f1 and f2 (f2 = 0xFFFFFFFF: none) of every record starting at a
  * multiple of `stride`, issued right after the 8-KiB piece holding the record's first byte has
- * been read.  Overwrites those bytes.  The time an in-place emit of the same batch cannot beat. */
+ * been read.  Overwrites those bytes.  The floor of an emit that stores its fields as 2-byte
+ * writes (fixed-stride emit writes whole 64-byte field segments where it can, and runs under it). */
 int smol_csum_tool_field_probe(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, uint64_t stride,
                                uint32_t f1, uint32_t f2, void* stream);
 /* The launch shape the library picks for a verify over an implicit batch of `len`-byte records. */
