@@ -193,8 +193,13 @@ int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
  * filled).  An ICMPv4 DstUnreachable / TimeExceeded message's embedded IPv4 header gets its header
  * checksum first, under caps.ipv4, as Icmpv4Repr::emit writes it with Ipv4Repr::emit
  * (src/wire/icmpv4.rs:520-543).  `d_status` (nullable) receives SMOL_ST_MALFORMED /
- * SMOL_ST_UNSUPPORTED per record.  One kernel on `stream`; records must not overlap.  No device
- * memory is allocated: the calls may be captured in a HIP graph. */
+ * SMOL_ST_UNSUPPORTED per record.  One kernel on `stream`; records must not overlap.  On a
+ * fixed-stride batch the kernel writes the 64-byte segment around an IPv4 record's fields whole
+ * where that is race-free within the call: the segment's other bytes, which may belong to the
+ * neighbouring records, are written back with the values the kernel read.  Bytes outside the
+ * batch's records are never written.  So nothing else may write the batch's records while the
+ * call runs, the same rule copy-emit states.  No device memory is allocated: the calls may be
+ * captured in a HIP graph. */
 int smol_csum_batch_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                          const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
 
