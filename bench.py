@@ -182,12 +182,35 @@ class Workload:
             eng.corrupt(self.rx, self.batch, every=64, seed=seed)
         self.status = torch.empty(self.n, dtype=torch.uint8, device=dev)
         self.est = None
-        # emit's floor probe: (record spacing, field offsets) — IPv4 header + UDP / TCP checksum;
-        # C4 one L4 field (UDP's offset; TCP's and ICMPv6's sit in the same first line); C3 at the
-        # mean record spacing (the same bytes and the same number of store events)
-        self.probe_fields = {"c2": (1500, 10, 26), "c5": (1500, 10, 26), "c2copy": (1500, 10, 26),
-                             "c4": (1320, 46, 0xFFFFFFFF),
-                             "c3": (max(16, self.total // max(self.n, 1)), 10, 36)}[cfg]
+        # emit's floor probe on fixed-stride IPv4 batches: (record stride, field offsets) — the IPv4
+        # header checksum and the UDP checksum; C3 / C4 list their fields from the headers (field_addrs)
+        self.probe_fields = (1500, 10, 26)
+
+
+def field_addrs(wl):
+    """Ascending byte offsets (int64, on the device) of the checksum fields emit fills in wl.tx: the
+    IPv4 header checksum and the L4 checksum of each record (KIND_IP records without extension
+    headers, as the synthetic profiles make them).  For emit's floor probe."""
+    import torch
+
+    b = wl.tx
+    if wl.batch.desc is None:
+        offs = torch.arange(wl.n, device=b.device, dtype=torch.int64) * wl.batch.stride
+    else:
+        offs = wl.batch.desc.view(torch.int64).view(wl.n, 2)[:, 0].clone()
+    b0 = b[offs].to(torch.int64)
+    v4 = (b0 >> 4) == 4
+    ihl = (b0 & 15) * 4
+    proto = torch.where(v4, b[offs + 9].to(torch.int64), b[offs + 6].to(torch.int64))
+    l4 = torch.where(v4, offs + ihl, offs + 40)
+    fo = torch.full_like(offs, -1)
+    fo = torch.where(proto == 17, 6, fo)
+    fo = torch.where(proto == 6, 16, fo)
+    fo = torch.where((proto == 1) | (proto == 58), 2, fo)
+    ip = offs[v4] + 10
+    l4f = (l4 + fo)[fo >= 0]
+    a, _ = torch.sort(torch.cat([ip, l4f]))
+    return a
 
 
 # ---------------------------------------------------------------------------------------------
@@ -644,19 +667,41 @@ def main(argv=None):
             return a.elapsed_time(b) / reps
 
         ro_ms = timed(lambda: eng.stream_read(wl.tx, sink, stream=stream))
-        stride, f1, f2 = wl.probe_fields
-        fp_ms = timed(lambda: eng.field_probe(wl.tx, stride, f1, f2, stream=stream))
-        eng.emit(wl.tx, wl.batch, stream=stream)  # the probe overwrote the fields: emit them again
+        # the probe stores into wl.tx: the bytes it overwrites are saved first and put back after it
+        # (emit is not a restore: on C3 / C4 the probe's offsets are not all checksum fields)
+        addrs = field_addrs(wl)
+        nb = wl.tx.numel() // 16 * 16
+        pieces = torch.arange(0, (nb + 8191) // 8192 + 1, device=dev, dtype=torch.int64) * 8192
+        first = torch.searchsorted(addrs, pieces).to(torch.int32)
+        del pieces
+        saved = torch.stack([wl.tx[addrs], wl.tx[addrs + 1]])
+        if wl.batch.desc is None and wl.cfg != "c4":
+            stride, f1, f2 = wl.probe_fields
+            fp_ms = timed(lambda: eng.field_probe(wl.tx, stride, f1, f2, stream=stream))
+            where = (f"a 2-B store at offsets {f1}" + (f" and {f2}" if f2 != 0xFFFFFFFF else "")
+                     + f" of every {stride}-B record")
+        else:
+            fp_ms = timed(lambda: eng.field_probe_list(wl.tx, addrs, first, stream=stream))
+            where = f"a 2-B store at each of the {addrs.numel()} checksum fields of the records (from their headers)"
+        wl.tx[addrs] = saved[0]
+        wl.tx[addrs + 1] = saved[1]
+        del saved
+        # the same stream with the 64-B segment around each field rewritten whole (values unchanged):
+        # the store shape of whole-segment emit, every segment, no race check
+        seg_ms = timed(lambda: eng.field_probe_list(wl.tx, addrs, first, seg64=True, stream=stream))
+        del addrs, first
         torch.cuda.synchronize()
         nbytes = wl.tx.numel() // 16 * 16
         probe = {"kernel": "stream_read_kernel", "bytes": nbytes, "ms": round(ro_ms, 4),
                  "GB/s": round(nbytes / ro_ms / 1e6, 1)}
         floor = {"kernel": "field_probe_kernel", "ms": round(fp_ms, 4), "read_only_ms": round(ro_ms, 4),
-                 "what": f"the TX buffer streamed once (best read pattern) + a 2-B store at offsets {f1}"
-                         + (f" and {f2}" if f2 != 0xFFFFFFFF else "") + f" of every {stride}-B record "
-                         "(emit's store events as 2-B writes, no parse / gates): the floor of an emit that "
-                         "stores its fields as 2-B writes; whole 64-B field segments (fixed-stride emit, "
-                         "variant 19) run under it"}
+                 "what": "the 2-B-store reference: the TX buffer streamed once (best read pattern) + " + where
+                         + " (emit's store events as 2-B writes, no parse / gates); fixed-stride emit writes "
+                         "whole 64-B field segments (variant 19) and runs under it; the bytes the probe "
+                         "overwrote are restored",
+                 "seg64_ms": round(seg_ms, 4),
+                 "seg64_what": "the same stream with the 64-B segment holding each checksum field rewritten "
+                               "whole (its own values): the floor of a whole-segment emit"}
 
     unfused = None
     if wl.copy is not None and rank == 0:
@@ -741,6 +786,14 @@ def main(argv=None):
         if floor and dom == "emit":
             out["roofline"]["floor"] = floor
             out["roofline"]["floor_frac"] = round(floor["ms"] / kd["ms"], 4)
+        if probe and dom in ("emit", "verify"):
+            # the dominant kernel against the read-only stream over the same bytes (1.0 = it runs at
+            # the speed of reading its input once at the best pattern)
+            out["roofline"]["read_only_frac"] = round(probe["ms"] / kd["ms"], 4)
+        # the whole step against the HBM peak: algorithmic bytes of both kernels / wall time per step
+        step_bytes = sum(v["bytes"] for v in kernels.values())
+        out["roofline"]["step_frac"] = round(step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
+        out["roofline"]["step_algorithmic_bytes"] = step_bytes
         if unfused:
             out["unfused_tx"] = unfused
         print(json.dumps(out), flush=True)

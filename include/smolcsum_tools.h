@@ -79,6 +79,13 @@ int smol_csum_tool_stream_read(smol_csum_ctx_t* ctx, const uint8_t* d_buf, uint6
  * writes (fixed-stride emit writes whole 64-byte field segments where it can, and runs under it). */
 int smol_csum_tool_field_probe(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, uint64_t stride,
                                uint32_t f1, uint32_t f2, void* stream);
+/* The same probe with the store addresses listed (descriptor batches): `d_addrs` holds ascending
+ * byte offsets into the buffer of 2-byte stores, and `d_piece_first[j]` the index of the first of them
+ * at or after byte 8192 * j, for j = 0 .. ceil(bytes / 8192) (that many + 1 entries).  Overwrites
+ * the bytes at those offsets.  `flags` bit 0: instead rewrite the whole 64-byte segment holding each
+ * offset with the values it holds (the store shape of whole-segment emit; nothing changes). */
+int smol_csum_tool_field_probe_list(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
+                                    const uint32_t* d_piece_first, int flags, void* stream);
 /* The launch shape the library picks for a verify over an implicit batch of `len`-byte records. */
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc);
 

@@ -169,15 +169,18 @@ def nhc_udp_checksum(src: bytes, dst: bytes, sport: int, dport: int, payload: by
 
 def nhc_udp_verify(p: bytes, src: bytes, dst: bytes):
     """UdpNhcRepr::parse's checksum test (nhc.rs:697-723): None when the packet is dropped before
-    it (check_len, dispatch), else whether the inline checksum (if any) matches."""
+    it (check_len, dispatch, or the destination port 0 that the iface's UdpRepr::parse of the
+    decompressed header drops), else whether the inline checksum (if any) matches."""
     if len(p) < 1:
         return None
     ports, cs = _nhc_sizes(p[0])
     if 1 + ports + cs > len(p) or (p[0] >> 3) != 0x1E:
         return None
+    sport, dport = nhc_ports(p)
+    if dport == 0:  # dropped by UdpRepr::parse after decompression (sixlowpan.rs:745-775, udp.rs:246-248)
+        return None
     if cs == 0:
         return True
-    sport, dport = nhc_ports(p)
     return nhc_udp_checksum(src, dst, sport, dport, p[1 + ports + cs:]) == (p[1 + ports] << 8 | p[2 + ports])
 
 

@@ -95,10 +95,13 @@ int walk_variant(int mode, bool has_desc) {
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
-bool line_grid(int variant) { return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 19; }
+bool line_grid(int variant) {
+    return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 19 ||
+           (variant >= 23 && variant <= 27);
+}
 
 int auto_shape(uint32_t len, bool has_desc, bool line = false, int variant = -1) {
-    if (has_desc) return variant == 13 ? CFG_G16U4 : CFG_G16U3;
+    if (has_desc) return (variant == 13 || variant == 26 || variant == 27) ? CFG_G16U4 : CFG_G16U3;
     const uint64_t need = (uint64_t)len + (line ? 127 : 15);  // bytes of aligned chunks a record can touch
     // eight records per wavefront in two steps, with as few idle lanes as possible (C4's 1320-B
     // records on the line grid: 8 x 6 0.2083 ms, 8 x 7 0.2188 ms; C2's 1500 B: 8 x 7 0.2327 ms)
@@ -384,7 +387,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 19) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 27) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }
@@ -419,6 +422,17 @@ int smol_csum_tool_field_probe(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t by
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
     hipError_t e = launch_field_probe(d_buf, bytes, stride, f1, f2, (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * 8u,
                                       (hipStream_t)stream);
+    return e == hipSuccess ? SMOL_OK : hip_fail(e, "field-probe kernel launch");
+}
+
+int smol_csum_tool_field_probe_list(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
+                                    const uint32_t* d_piece_first, int flags, void* stream) {
+    if (!ctx || !d_buf || !d_addrs || !d_piece_first || (bytes & 15u) || ((uintptr_t)d_buf & 15u) || (flags & ~1))
+        return SMOL_EINVAL;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    hipError_t e = launch_field_probe_list(d_buf, bytes, d_addrs, d_piece_first, flags & 1,
+                                           (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * 8u, (hipStream_t)stream);
     return e == hipSuccess ? SMOL_OK : hip_fail(e, "field-probe kernel launch");
 }
 

@@ -128,6 +128,12 @@ __device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint3
         const uint32_t ps = (b0 & 3u) == 0 ? 4u : (b0 & 3u) == 3 ? 1u : 3u;  // ports_size :602-611
         const uint32_t cs = (emit || !(b0 & 4u)) ? 2u : 0u;                     // checksum_size :593-599
         if (1 + ps + cs > len || (b0 >> 3) != 0x1eu) { g.st = SMOL_ST_MALFORMED; return g; }
+        // verify: destination port 0 (inline in ports modes 0b00 / 0b10) is dropped by UdpRepr::parse
+        // of the decompressed header (src/iface/interface/sixlowpan.rs:745-775, udp.rs:246-248)
+        if (!emit && ((b0 & 3u) == 0 || (b0 & 3u) == 2)) {
+            const uint32_t dp = (b0 & 3u) == 0 ? (rd(3) << 8 | rd(4)) : (rd(2) << 8 | rd(3));
+            if (dp == 0) { g.st = SMOL_ST_MALFORMED; return g; }
+        }
         g.proto = P_NHC_UDP;
         g.l4_off = 1 + ps + cs;
         g.l4_len = len - g.l4_off;

@@ -60,14 +60,24 @@ namespace smolcsum {
 // the record written (WHOLE, see walk_step).  Measured variants that lost are in DESIGN.md §6.
 template <int VAR>
 struct VarT {
-    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19;
-    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16;
-    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19;
+    static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
+                               (VAR >= 23 && VAR <= 27);
+    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 26 && VAR != 27;
+    static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
+                                 (VAR >= 23 && VAR <= 27);
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
     static constexpr bool SHUF2 = VAR == 16;
     static constexpr bool SEGW = VAR == 19;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
+    // 23-27 (emit): whole 64-B field segments with the neighbours' record extents published too, so
+    // that they serve descriptor batches as well as fixed strides (SEGG); SEGB: the neighbours of the
+    // whole workgroup, not only of the wavefront (a workgroup barrier after the parse, natural grid);
+    // SEG6: IPv6 records too.  23 = 5 + SEGG + SEGB + SEG6, 24 = 23 without SEGB, 25 = 23 without
+    // SEG6, 26 = 13 (no prefetch) + SEGG + SEGB + SEG6, 27 = 26 without SEGB.
+    static constexpr bool SEGG = VAR >= 23 && VAR <= 27;
+    static constexpr bool SEGB = VAR == 23 || VAR == 25 || VAR == 26;
+    static constexpr bool SEG6 = VAR == 23 || VAR == 24 || VAR == 26 || VAR == 27;
 };
 
 template <bool LINE>
@@ -354,6 +364,15 @@ struct SegInfo {
     uint32_t tag2, lo;  // read by the previous group
 };
 
+// SEGG: the same with the record's extent, so that a neighbour can tell whether the bytes of a
+// segment outside its own record belong to this record (descriptor batches: records anywhere).
+// All addresses absolute; [flo, fhi) = the fields' byte range (flo = ~0, fhi = 0: none).
+struct SegInfoG {
+    uint32_t tag, pad;
+    uint64_t beg, end;
+    uint64_t flo, fhi;
+};
+
 // The record offsets of the fields emit may write (NO_FIELD: none): a superset of finish_gates'.
 __device__ __forceinline__ void emit_fields(const Geom& g, uint32_t f[3]) {
     f[0] = g.fam == 4 ? g.ip_off + 10 : NO_FIELD;
@@ -577,10 +596,12 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 // One step of the walk: prefetch the following step into `nx`, then sum `cv` (the current step)
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
-          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false, bool SEGW = false>
+          bool SHUF = false, bool WHOLE = false, bool SHUF2 = false, bool SEGW = false, bool SEGG = false,
+          bool SEGB = false, bool SEG6 = false>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
-                                          int gib, SegInfo* si = nullptr) {
+                                          int gib, SegInfo* si = nullptr, SegInfoG* sg = nullptr,
+                                          bool blockwide = false) {
     constexpr bool COPY = MODE == MODE_COPY;
     // where the record geometry lives (Walk::g / Walk::gr): registers for emit with the register
     // prefetch, LDS otherwise
@@ -781,7 +802,69 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                     if (whole(rA)) w.segA = rA;
                     if (rB != rA && whole(rB)) w.segB = rB;
                 }
-            }        }
+            }
+            if constexpr (SEGG) {
+                // publish the record's extent and every field finish_gates may write (a superset is
+                // safe), then decide which of this record's field segments go out whole
+                uint32_t f[3], lo = NO_FIELD, hi = 0;
+                emit_fields(g, f);
+                for (int j = 0; j < 3; ++j)
+                    if (f[j] != NO_FIELD) {
+                        lo = f[j] < lo ? f[j] : lo;
+                        hi = f[j] + 2 > hi ? f[j] + 2 : hi;
+                    }
+                const uint64_t a0 = w.cur.a0, a1 = w.cur.a0 + w.cur.len;
+                if (lane == 0) {
+                    SegInfoG e;
+                    e.tag = (uint32_t)w.r;
+                    e.pad = 0;
+                    e.beg = a0;
+                    e.end = a1;
+                    e.flo = lo != NO_FIELD ? a0 + lo : ~0ull;
+                    e.fhi = lo != NO_FIELD ? a0 + hi : 0ull;
+                    sg[gib] = e;
+                }
+                // SEGB: every group of the workgroup is on its first (and only) record here, so one
+                // barrier makes every neighbour's entry visible (blockwide is uniform over the
+                // workgroup: a natural grid and a full workgroup, see csum_kernel)
+                if (SEGB && blockwide) __syncthreads();
+                else wave_lds_sync();
+                w.segA = w.segB = SEG_NONE;
+                const bool fam_ok = g.fam == 4 || (SEG6 && g.fam == 6);
+                if (fam_ok && lo != NO_FIELD && p.n < 0xFFFFFFFFull && w.cur.len < (1u << 29)) {
+                    constexpr int GPW = 64 / G;
+                    const uint64_t r = w.r;
+                    const bool have_prev = (SEGB && blockwide) ? gib > 0 : (gib % GPW) != 0;
+                    const bool have_next = (SEGB && blockwide) ? gib + 1 < 256 / G : (gib % GPW) != GPW - 1;
+                    // the previous record's extent and last field byte, the next one's (valid only
+                    // when its group holds record r -/+ 1 right now: the tag check)
+                    bool pv = false, nv = false;
+                    uint64_t pbeg = 0, pfhi = 0, nend = 0, nflo = 0;
+                    if (have_prev && r > 0) {
+                        const SegInfoG q = sg[gib - 1];
+                        pv = q.tag == (uint32_t)(r - 1) && q.end == a0;
+                        pbeg = q.beg;
+                        pfhi = q.fhi;
+                    }
+                    if (have_next && r + 1 < p.n) {
+                        const SegInfoG q = sg[gib + 1];
+                        nv = q.tag == (uint32_t)(r + 1) && q.beg == a1;
+                        nend = q.end;
+                        nflo = q.flo;
+                    }
+                    const uint64_t SA = (a0 + lo) & ~63ull, SB = (a0 + hi - 1) & ~63ull;
+                    // the window holds the record's chunks only (past its last one: the dummy line)
+                    const uint64_t wend = base + 16ull * (w.nch < (uint32_t)WIN_CH ? w.nch : (uint32_t)WIN_CH);
+                    auto whole = [&](uint64_t S) {
+                        return SB <= SA + 64 && S + 64 <= wend &&
+                               (S >= a0 || (pv && pbeg <= S && pfhi <= S)) &&
+                               (S + 64 <= a1 || (nv && nend >= S + 64 && nflo >= S + 64));
+                    };
+                    if (whole(SA)) w.segA = (int32_t)(int64_t)(SA - a0);
+                    if (SB != SA && whole(SB)) w.segB = (int32_t)(int64_t)(SB - a0);
+                }
+            }
+        }
     }
     // MODE_COPY: store the payload bytes of this step (all of them, summed or not).  WHOLE: store
     // every byte of the record instead (the bytes outside the payload unchanged), so that no cache
@@ -884,14 +967,14 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             // records and the window holds all of it.  Fields outside such segments are stored as
             // 2-B fields.
             uint64_t wsA = ~0ull, wsB = ~0ull;
-            if constexpr (SEGW) {  // the segments decided after the parse (step 0)
+            if constexpr (SEGW || SEGG) {  // the segments decided after the parse (step 0)
                 if (w.segA != SEG_NONE) wsA = w.cur.a0 + (int64_t)w.segA;
                 if (w.segB != SEG_NONE) wsB = w.cur.a0 + (int64_t)w.segB;
             }
-            finish_gates<G, MODE, NHC, decltype(rd), ((COPY && WHOLE) || SEGW) ? WIN : 0, SEGW>(
+            finish_gates<G, MODE, NHC, decltype(rd), ((COPY && WHOLE) || SEGW || SEGG) ? WIN : 0, SEGW || SEGG>(
                 p, GREG ? w.gr : *w.g, w.acc, rd, winb, head, w.cur.a0, r, lane, reinterpret_cast<uint8_t*>(win),
                 wsA, wsB);
-            if constexpr (SEGW) {
+            if constexpr (SEGW || SEGG) {
                 if (wsA != ~0ull || wsB != ~0ull) {
                     wave_lds_sync();
                     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -966,7 +1049,11 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     __shared__ u32x4 win[GPB][Grid<LINE>::WIN_CH];
     __shared__ Geom geo[GPB];
     constexpr bool SEGW = VarT<VAR>::SEGW && MODE == MODE_EMIT && IMPLICIT && LINE && !NHC;
+    constexpr bool SEGG = VarT<VAR>::SEGG && MODE == MODE_EMIT && LINE && !NHC;
+    constexpr bool SEGB = SEGG && VarT<VAR>::SEGB;
+    constexpr bool SEG6 = SEGG && VarT<VAR>::SEG6;
     __shared__ SegInfo segi[SEGW ? GPB : 1];
+    __shared__ SegInfoG segg[SEGG ? GPB : 1];
 
     const int lane = (int)(threadIdx.x % G);
     const int gib = (int)(threadIdx.x / G);
@@ -974,6 +1061,12 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
     if constexpr (SEGW) {
         if (lane == 0) segi[gib].tag = segi[gib].tag2 = ~0u;  // no record yet (read by the neighbours)
     }
+    if constexpr (SEGG) {
+        if (lane == 0) segg[gib].tag = ~0u;
+    }
+    // SEGB: a natural grid (one record per group) and a full workgroup, the same for every wave of
+    // the workgroup, so that each of them reaches the barrier after the parse exactly once
+    const bool blockwide = SEGB && ngroups >= p.n && (uint64_t)blockIdx.x * GPB + GPB <= p.n;
     Walk w;
     w.r = (uint64_t)blockIdx.x * GPB + gib;
     if (w.r >= p.n) return;
@@ -999,14 +1092,17 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
                                                   shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6>(
+                    p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6>(
+                    p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
         }
     } else {
         while (true) {
             load_step<G, U, NT, COPY, LINE, 0, SHUF, SHUF2>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
                                                             shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF, WHOLE, SHUF2>(p, w, va, va, lane, ngroups, &win[gib][0], gib)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF, WHOLE, SHUF2, false, SEGG, SEGB, SEG6>(
+                    p, w, va, va, lane, ngroups, &win[gib][0], gib, nullptr, segg, blockwide)) break;
         }
     }
 }
@@ -1039,6 +1135,23 @@ hipError_t launch_shape(int shape, const KParams& p, uint32_t max_blocks, hipStr
     }
 }
 
+// The whole-segment emit variants (23-27) are built for the shapes emit picks (8 x 6 / 8 x 7 at a
+// fixed stride, 16 x 3 / 16 x 4 over descriptors) and 32 x 4 / 64 x 4 for long records; the other
+// shapes map to the one with the same group size.
+template <bool IMPLICIT, int VAR>
+hipError_t launch_seg_shape(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    switch (shape) {
+        case CFG_G8U6: return launch_one<8, 6, MODE_EMIT, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G8U7: return launch_one<8, 7, MODE_EMIT, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G16U3: return launch_one<16, 3, MODE_EMIT, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G16U4:
+        case CFG_G16U6: return launch_one<16, 4, MODE_EMIT, IMPLICIT, VAR>(p, max_blocks, s);
+        case CFG_G32U3:
+        case CFG_G32U4: return launch_one<32, 4, MODE_EMIT, IMPLICIT, VAR>(p, max_blocks, s);
+        default: return launch_one<64, 4, MODE_EMIT, IMPLICIT, VAR>(p, max_blocks, s);
+    }
+}
+
 template <int MODE, bool IMPLICIT>
 hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (var) {
@@ -1048,6 +1161,22 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
         case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
         case 19: return launch_shape<MODE, IMPLICIT, 19>(shape, p, max_blocks, s);
+        case 23:
+        case 24:
+        case 25:
+        case 26:
+        case 27:
+            if constexpr (MODE == MODE_EMIT) {
+                switch (var) {
+                    case 23: return launch_seg_shape<IMPLICIT, 23>(shape, p, max_blocks, s);
+                    case 24: return launch_seg_shape<IMPLICIT, 24>(shape, p, max_blocks, s);
+                    case 25: return launch_seg_shape<IMPLICIT, 25>(shape, p, max_blocks, s);
+                    case 26: return launch_seg_shape<IMPLICIT, 26>(shape, p, max_blocks, s);
+                    default: return launch_seg_shape<IMPLICIT, 27>(shape, p, max_blocks, s);
+                }
+            }
+            return var >= 26 ? launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s)
+                             : launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 9:
         case 10:
             if constexpr (MODE == MODE_EMIT && IMPLICIT) {
@@ -1066,7 +1195,7 @@ template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
     // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
-    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19) {
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 27)) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);

@@ -290,6 +290,64 @@ __global__ __launch_bounds__(256) void field_probe_kernel(uint8_t* buf, uint64_t
     }
 }
 
+// The same probe with the store addresses given as a list (descriptor batches, whose fields do not
+// sit at a fixed spacing): addrs[] ascending byte offsets of 2-byte stores, first[j] the index of the
+// first address inside the 8-KiB piece j (first[] has ceil(bytes / 8 KiB) + 1 entries).
+// seg64: rewrite the whole 64-B segment holding each address instead (with the values it holds:
+// loaded by the storing lane, an L2 hit after the piece's stream) — the store shape of variant 19.
+__global__ __launch_bounds__(256) void field_probe_list_kernel(uint8_t* buf, uint64_t n16, const uint64_t* addrs,
+                                                               const uint32_t* first, int seg64) {
+    constexpr int UNR = 8;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const uint64_t per = 64ull * UNR;
+    const uint64_t bytes = n16 * 16;
+    const u32x4s* q = reinterpret_cast<const u32x4s*>(buf);
+    auto stores = [&](uint64_t piece, uint32_t acc) {
+        const uint32_t i0 = first[piece], i1 = first[piece + 1];
+        for (uint32_t i = i0 + (uint32_t)lane; i < i1; i += 64) {
+            if (seg64) {
+                const uint64_t a = addrs[i] & ~63ull;
+                if (a + 64 <= bytes) {
+                    typedef __attribute__((address_space(1))) u32x4s* gv4;
+                    const gv4 g = (gv4)(buf + a);
+                    const u32x4s x0 = g[0], x1 = g[1], x2 = g[2], x3 = g[3];
+                    g[0] = x0;
+                    g[1] = x1;
+                    g[2] = x2;
+                    g[3] = x3;
+                }
+            } else {
+                probe_store(buf, bytes, addrs[i], acc + i);
+            }
+        }
+    };
+    for (uint64_t base = w0 * per; base + per <= n16; base += nw * per) {
+        u32x4s v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) v[u] = __builtin_nontemporal_load(q + base + u * 64 + lane);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+            acc += __builtin_amdgcn_sad_u16(v[u].x, 0, 0) + __builtin_amdgcn_sad_u16(v[u].y, 0, 0) +
+                   __builtin_amdgcn_sad_u16(v[u].z, 0, 0) + __builtin_amdgcn_sad_u16(v[u].w, 0, 0);
+        stores(base / per, acc);
+    }
+    const uint64_t tail = n16 / per * per;
+    if (w0 == 0 && tail < n16) {
+        uint32_t acc = 0;
+        for (uint64_t i = tail + (uint64_t)lane; i < n16; i += 64) acc += q[i].x;
+        stores(tail / per, acc);
+    }
+}
+
+hipError_t launch_field_probe_list(uint8_t* buf, uint64_t bytes, const uint64_t* addrs, const uint32_t* first,
+                                   int seg64, uint32_t max_blocks, hipStream_t s) {
+    hipLaunchKernelGGL(field_probe_list_kernel, dim3(max_blocks), dim3(256), 0, s, buf, bytes / 16, addrs, first, seg64);
+    return hipGetLastError();
+}
+
 hipError_t launch_field_probe(uint8_t* buf, uint64_t bytes, uint64_t stride, uint32_t f1, uint32_t f2,
                               uint32_t max_blocks, hipStream_t s) {
     hipLaunchKernelGGL(field_probe_kernel, dim3(max_blocks), dim3(256), 0, s, buf, bytes / 16, stride, f1, f2);

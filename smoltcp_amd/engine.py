@@ -291,6 +291,18 @@ class ChecksumEngine:
         check(lib().smol_csum_tool_field_probe(self._h, buf.data_ptr(), nbytes, int(stride), int(f1), int(f2),
                                                self._stream(stream)), "smol_csum_tool_field_probe")
 
+    def field_probe_list(self, buf, addrs, piece_first, seg64: bool = False, stream=None):
+        """Emit's floor probe with listed store addresses (tooling, smol_csum_tool_field_probe_list):
+        `addrs` a device u64 tensor of ascending byte offsets, `piece_first` a device u32 tensor with
+        the index of the first address at or after each 8-KiB piece (ceil(bytes / 8192) + 1
+        entries).  Overwrites the bytes at those offsets; with `seg64` rewrites the 64-B segments
+        holding them whole, with their own values, instead."""
+        nbytes = buf.numel() // 16 * 16
+        check(lib().smol_csum_tool_field_probe_list(self._h, buf.data_ptr(), nbytes, addrs.data_ptr(),
+                                                    piece_first.data_ptr(), int(bool(seg64)),
+                                                    self._stream(stream)),
+              "smol_csum_tool_field_probe_list")
+
     def set_shape(self, shape: int):
         check(lib().smol_csum_tool_set_shape(self._h, int(shape)), "smol_csum_tool_set_shape")
 

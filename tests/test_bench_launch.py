@@ -27,7 +27,7 @@ def _json_line(out: str):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
 def test_dry_run_launches_n_ranks(n):
     r = _run(["--gpus", str(n), "--dry-run", "--steps", "3", "--warmup", "1"])
     assert r.returncode == 0, r.stderr
@@ -89,6 +89,8 @@ def test_bench_gpu_contract():
     assert rl["bound"] == "hbm" and rl["unit"] == "GB/s" and rl["peak"] == 8000.0
     assert 0 < rl["frac"] < 1 and abs(rl["achieved"] / rl["peak"] - rl["frac"]) < 1e-3
     assert rl["floor"]["kernel"] == "field_probe_kernel" and 0 < rl["floor_frac"]
+    assert 0 < rl["read_only_frac"] and 0 < rl["step_frac"] < 1
+    assert rl["step_algorithmic_bytes"] == sum(k["algorithmic_bytes_per_launch"] for k in d["kernels_roofline"].values())
     n64 = d["config"]["records_per_gpu"] // 64  # 1/64 single-bit flips (a few the gates cannot see)
     assert d["ramp"]["steps"] >= 8 and n64 - 16 <= d["verify_rejected"] <= n64
     assert d["cpu_baseline"] is None  # --cpu-seconds 0

@@ -4,7 +4,8 @@ the oracle's restatement of UdpNhcRepr::emit / ::parse (src/wire/sixlowpan/nhc.r
 Covered: the reference's own datagram (tests/golden/kat.json ``sixlowpan_nhc_udp``, checksum
 0xb46b) through verify and through emit over a zeroed / elided checksum; random records of every
 port mode with inline and elided checksums, payloads 0..1999 B (odd payload offsets), records cut
-inside the header and other NHC dispatches (MALFORMED, untouched); packed descriptor batches with
+inside the header and other NHC dispatches (MALFORMED, untouched), inline destination port 0
+(MALFORMED on verify: the iface's UdpRepr::parse of the decompressed header drops it); packed descriptor batches with
 odd offsets and fixed-stride batches (line-grid emit with shared boundary lines, stride >= 384);
 every caps.udp value; every launch shape and kernel variant (the tile variants run the walk
 kernel); a persistent grid.
@@ -40,6 +41,9 @@ def _records(rng, n, max_payload=2000):
             r = r[: int(rng.integers(0, 1 + P.NHC_PORTS_SIZE[mode] + 2))]
         if i % 29 == 7 and r:
             r[0] = 0xE0 | (r[0] & 7)
+        if i % 11 == 2 and mode in (0, 2) and len(r) >= 5:  # inline destination port 0: MALFORMED on verify
+            r[3 if mode == 0 else 2] = 0
+            r[4 if mode == 0 else 3] = 0
         recs.append(bytes(r))
     return recs
 

@@ -70,6 +70,9 @@ def random_records(rng, n):
             r = r[: int(rng.integers(0, 1 + P.NHC_PORTS_SIZE[mode] + 2))]
         if i % 29 == 0 and r:
             r[0] = 0xE0 | (r[0] & 7)
+        if i % 7 == 3 and mode in (0, 2) and len(r) >= 5:  # destination port 0 (inline)
+            r[3 if mode == 0 else 2] = 0
+            r[4 if mode == 0 else 3] = 0
         recs.append(bytes(r))
     return recs
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Experiment: emit with the fields' 64-B segments written whole (variant 19) against variant 5,
-on C2 and C4 at steady clocks, interleaved; both must leave the same bytes.
-Usage: exp_emit_seg.py [c2,c4]"""
+"""Experiment: emit variants (whole 64-B field segments: 19, 23-27; 2-B stores: 5, 13; the tile
+kernel: 7) on C2 / C3 / C4 at steady clocks, interleaved rounds on one box; every variant must leave
+the same bytes as the first one listed.
+Usage: [VARS=5,19,23] [VARS_c3=7,26,27] [K=30] exp_emit_seg.py [c2,c4,c3]"""
 import json
 import os
 import sys
@@ -22,16 +23,25 @@ def main():
     eng = E.ChecksumEngine(0)
     wls = {c: bench.Workload(E, eng, c, 0, 0, dev) for c in cfgs}
     torch.cuda.synchronize()
-    for c, wl in wls.items():  # same bytes from both variants
-        outs = []
-        for v in (5, 19):
+    def vars_of(c):
+        return [int(x) for x in os.environ.get(f"VARS_{c}", os.environ.get("VARS", "5,19")).split(",")]
+
+    for c, wl in wls.items():  # the same bytes from every variant
+        ref = None
+        for v in vars_of(c):
             t = wl.tx.clone()
             eng.set_variant(v)
             eng.emit(t, wl.batch)
             torch.cuda.synchronize()
-            outs.append(t)
-        print(json.dumps({"cfg": c, "identical": bool(torch.equal(outs[0], outs[1]))}), flush=True)
-        del outs
+            if ref is None:
+                ref = t
+            else:
+                same = bool(torch.equal(ref, t))
+                print(json.dumps({"cfg": c, "variant": v, "identical_to_first": same}), flush=True)
+                if not same:
+                    raise SystemExit(f"{c}: variant {v} differs from variant {vars_of(c)[0]}")
+                del t
+        del ref
     eng.set_variant(-1)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.3:
@@ -39,10 +49,9 @@ def main():
             eng.emit(wl.tx, wl.batch)
         torch.cuda.synchronize()
     K = int(os.environ.get("K", "30"))
-    VARS = [int(x) for x in os.environ.get("VARS", "5,19").split(",")]
     for rnd in range(4):
         for c, wl in wls.items():
-            for v in VARS:
+            for v in vars_of(c):
                 eng.set_variant(v)
                 for _ in range(3):
                     eng.emit(wl.tx, wl.batch)
