@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SMOLCSUM_ABI_VERSION 4
+#define SMOLCSUM_ABI_VERSION 5
 
 /* ---- error codes ------------------------------------------------------------------------ */
 enum {
@@ -114,6 +114,15 @@ typedef struct {
  * SMOL_ST_MALFORMED when its IP header fails check_len.  In a fragment group the flag on any of
  * the group's records makes the whole datagram raw. */
 #define SMOL_REC_IPHDR_ONLY 0x01u
+
+/* Batch flag (smol_csum_batch_t.flags, fixed-stride and descriptor batches alike; ABI 5).
+ *
+ * SMOL_BATCH_FIELD_STORES — emit writes the checksum fields only (2-byte stores), never a whole
+ * 64-byte segment around them.  By default emit rewrites such segments, neighbouring records'
+ * bytes included, with the values it read (smol_csum_batch_emit below): a caller that writes other
+ * bytes of the batch's records from another stream while emit runs sets this flag.  Slower (one
+ * partial-line write per field). */
+#define SMOL_BATCH_FIELD_STORES 0x80u
 
 /* Batch geometry (host memory).  If `desc` is non-NULL it is a DEVICE array of `n` descriptors
  * and `stride`/`len`/`kind` are ignored.  Otherwise record i starts at base + i*stride, has
@@ -193,13 +202,14 @@ int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
  * filled).  An ICMPv4 DstUnreachable / TimeExceeded message's embedded IPv4 header gets its header
  * checksum first, under caps.ipv4, as Icmpv4Repr::emit writes it with Ipv4Repr::emit
  * (src/wire/icmpv4.rs:520-543).  `d_status` (nullable) receives SMOL_ST_MALFORMED /
- * SMOL_ST_UNSUPPORTED per record.  One kernel on `stream`; records must not overlap.  On a
- * fixed-stride batch the kernel writes the 64-byte segment around an IPv4 record's fields whole
- * where that is race-free within the call: the segment's other bytes, which may belong to the
- * neighbouring records, are written back with the values the kernel read.  Bytes outside the
- * batch's records are never written.  So nothing else may write the batch's records while the
- * call runs, the same rule copy-emit states.  No device memory is allocated: the calls may be
- * captured in a HIP graph. */
+ * SMOL_ST_UNSUPPORTED per record.  One kernel on `stream`; records must not overlap.  The kernel
+ * writes the 64-byte segment around a record's fields whole where that is race-free within the
+ * call: the segment's other bytes, which may belong to the records just before and after it in
+ * the batch (contiguous with it in memory, no field of theirs in the segment), are written back
+ * with the values the kernel read.  Bytes outside the batch's records are never written.  So
+ * nothing else may write the batch's records while the call runs, the same rule copy-emit states,
+ * unless the batch sets SMOL_BATCH_FIELD_STORES (fields only).  No device memory is allocated: the
+ * calls may be captured in a HIP graph. */
 int smol_csum_batch_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                          const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
 

@@ -95,6 +95,13 @@ int walk_variant(int mode, bool has_desc) {
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
+// SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
+int field_store_variant(int variant, bool has_desc) {
+    if (variant == 19 || variant == 23 || variant == 24 || variant == 25) return 5;
+    if (variant == 26 || variant == 27) return 13;
+    return variant;
+}
+
 bool line_grid(int variant) {
     return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 19 ||
            (variant >= 23 && variant <= 27);
@@ -116,7 +123,9 @@ int check_batch(const smol_csum_batch_t* b, const void* d_buf) {
     if (!b) return SMOL_EINVAL;
     if (b->n == 0) return SMOL_OK;
     if (!d_buf) return SMOL_EINVAL;
-    if ((b->flags & ~SMOL_REC_IPHDR_ONLY) != 0 || b->reserved[0] != 0 || b->reserved[1] != 0) return SMOL_EINVAL;
+    if ((b->flags & ~(SMOL_REC_IPHDR_ONLY | SMOL_BATCH_FIELD_STORES)) != 0 || b->reserved[0] != 0 ||
+        b->reserved[1] != 0)
+        return SMOL_EINVAL;
     if (b->desc) {
         if (((uintptr_t)b->desc & 15u) != 0) return SMOL_EINVAL;
     } else if (b->len > SMOL_MAX_RECORD_LEN) {
@@ -160,6 +169,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     int variant = ctx->variant;
     const bool has_desc = b->desc != nullptr;
     if (variant < 0) variant = auto_variant(mode, has_desc);
+    if (mode == MODE_EMIT && (b->flags & SMOL_BATCH_FIELD_STORES)) variant = field_store_variant(variant, has_desc);
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
     if (tile_var && (mode == MODE_DATA || mode == MODE_COPY || d_addrs)) variant = walk_variant(mode, has_desc);
     const bool use_tile = variant == 3 || variant == 4 || variant == 7;

@@ -21,6 +21,7 @@ from .phy import ChecksumCapabilities
 
 KIND_RAW, KIND_IP, KIND_ETH = 0, 1, 2
 REC_IPHDR_ONLY = 0x01  # SMOL_REC_IPHDR_ONLY: a raw socket's frame (the IP header's gate only)
+BATCH_FIELD_STORES = 0x80  # SMOL_BATCH_FIELD_STORES: emit stores the checksum fields only (no whole segments)
 
 ST_IP_OK = 0x01
 ST_L4_OK = 0x02
@@ -86,7 +87,7 @@ class Batch:
     length: int = 0
     kind: int = KIND_IP
     desc: Optional[object] = None  # torch.Tensor (uint8, device) holding n descriptors
-    flags: int = 0                 # SMOL_REC_* of every record of a fixed-stride batch
+    flags: int = 0                 # SMOL_REC_* of every record of a fixed-stride batch, | SMOL_BATCH_*
 
     def c(self) -> BatchC:
         b = BatchC()
@@ -103,12 +104,13 @@ class Batch:
         return Batch(n=n, stride=stride, length=stride if length is None else length, kind=kind, flags=flags)
 
     @staticmethod
-    def from_records(offsets, lengths, kinds, device, flags=0) -> "Batch":
+    def from_records(offsets, lengths, kinds, device, flags=0, batch_flags: int = 0) -> "Batch":
+        """`flags`: SMOL_REC_* per record (descriptor flags); `batch_flags`: SMOL_BATCH_* of the batch."""
         import torch
 
         d = make_descriptors(offsets, lengths, kinds, flags)
         t = torch.from_numpy(d.view(np.uint8).copy()).to(device)
-        return Batch(n=len(d), desc=t)
+        return Batch(n=len(d), desc=t, flags=batch_flags)
 
 
 def _caps(caps) -> Caps:

@@ -244,3 +244,44 @@ def test_emit_write_set_concurrent(eng, gap):
         assert (out == K).all(), (variant, gap, np.nonzero(out != K)[0][:8])
         assert np.array_equal(got[pre: pre + n * stride].reshape(n, stride)[:, :L],
                               ref.reshape(n, stride)[:, :L]), (variant, gap)
+
+
+def test_field_stores_flag(eng):
+    """SMOL_BATCH_FIELD_STORES: emit stores the checksum fields only.  The output equals the
+    oracle's (fixed-stride and descriptor batches, every whole-segment variant forced), and bytes
+    of the records next to the fields that another stream rewrites while emit runs keep that
+    stream's last value."""
+    rng = np.random.default_rng(8)
+    recs = [_record(rng, i, 64, 600) for i in range(900)]
+    host, offs, lens = _layout(recs, np.arange(len(recs)), np.zeros(len(recs), int), rng, pad=21)
+    n = len(recs)
+    desc = P.oracle_desc(offs, lens, E.KIND_IP)
+    ref = host.copy()
+    oracle.batch_emit(ref, desc, n)
+    batch = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0", batch_flags=E.BATCH_FIELD_STORES)
+    for variant in (-1, 19, 23, 26, 27, 7):
+        d = torch.from_numpy(host.copy()).cuda()
+        eng.set_variant(variant)
+        try:
+            eng.emit(d, batch)
+            got = d.cpu().numpy()
+        finally:
+            eng.set_variant(-1)
+        assert np.array_equal(got, ref), (variant, np.nonzero(got != ref)[0][:8])
+    # a fixed-stride C2-like batch: UDP payload bytes 30..63 of every record (in the segment that
+    # holds the IPv4 header and UDP checksums) rewritten from another stream while emit runs
+    n, L = 1 << 15, 1500
+    buf = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+    fixed = E.Batch.fixed(n, L, L, E.KIND_IP, flags=E.BATCH_FIELD_STORES)
+    eng.synth(buf, fixed, E.SYNTH_UDP4, seed=5)
+    payload = buf[: n * L].view(n, L)[:, 30:64]
+    s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    K = 120
+    for k in range(1, K + 1):
+        with torch.cuda.stream(s_write):
+            payload.fill_(k)
+        if k % 12 == 1:
+            eng.emit(buf, fixed, stream=s_emit)
+    torch.cuda.synchronize()
+    assert bool((payload == K).all())

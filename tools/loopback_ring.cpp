@@ -10,11 +10,16 @@
 //   CPU inline:  the same fill + verify per frame with the scalar mirrors on one host thread
 //                (what smoltcp does in Ipv4Repr/TcpRepr::emit and ::parse with caps = Both).
 //
-//   loopback_ring [frames] [reps]      prints one JSON line
+//   loopback_ring [frames] [reps] [dump-prefix]      prints one JSON line
+//
+// With a dump prefix, every 97th frame of the last GPU pass is written out as built (zero checksum
+// fields: PREFIX.before), after OffloadRing::emit (PREFIX.after) and its verify status byte
+// (PREFIX.status), so that a test can compare them with the oracle byte for byte.
 //
 // Rates are frame bytes per second through the checksum stage (frame building excluded).
 #include <chrono>
 #include <cstdio>
+#include <string>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -97,6 +102,24 @@ int main(int argc, char** argv) {
             t_verify += std::chrono::duration<double>(t2 - t1).count();
         }
         for (uint32_t i = 0; i < n; ++i) accepted += smoltcp_amd::accepted(ring.status()[i]);
+        if (argc > 3) {  // the sample the oracle checks: frames as built, as emitted, their status
+            const std::string pre = argv[3];
+            FILE* fb = std::fopen((pre + ".before").c_str(), "wb");
+            FILE* fa = std::fopen((pre + ".after").c_str(), "wb");
+            FILE* fs = std::fopen((pre + ".status").c_str(), "wb");
+            if (!fb || !fa || !fs) throw std::runtime_error("cannot write the dump files");
+            std::vector<uint8_t> f(kFrame);
+            for (uint32_t i = 0; i < n; i += 97) {
+                std::memset(f.data(), 0, kFrame);
+                build_frame(f.data(), i * kMss, sockbuf.data() + (i % 64) * kMss);
+                std::fwrite(f.data(), 1, kFrame, fb);
+                std::fwrite(ring.slot(i), 1, kFrame, fa);
+                std::fwrite(ring.status() + i, 1, 1, fs);
+            }
+            std::fclose(fb);
+            std::fclose(fa);
+            std::fclose(fs);
+        }
         uint64_t cross = 0;  // the host gates agree with the GPU on the emitted frames
         for (uint32_t i = 0; i < n; i += 97) cross += cpu_verify(ring.slot(i));
         // ---- CPU inline (1 thread, scalar mirrors)
