@@ -134,11 +134,16 @@ def test_raw_records_fixed_stride_and_copy_emit(eng):
             eng.set_variant(-1)
     src = np.random.default_rng(5).integers(0, 256, n * 1472 + 16, dtype=np.uint8)
     copies = E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472)
-    d = torch.from_numpy(h.copy()).cuda()
-    eng.copy_emit(d, batch, torch.from_numpy(src).cuda(), torch.from_numpy(copies.view(np.uint8).copy()).cuda())
     ref = h.copy()
     oracle.batch_copy_emit(ref, None, n, src, copies, L, L, oracle.kind_flags(E.KIND_IP, E.REC_IPHDR_ONLY))
-    assert np.array_equal(d.cpu().numpy(), ref)
+    for variant in (-1, 17, 20):
+        eng.set_variant(variant)
+        try:
+            d = torch.from_numpy(h.copy()).cuda()
+            eng.copy_emit(d, batch, torch.from_numpy(src).cuda(), torch.from_numpy(copies.view(np.uint8).copy()).cuda())
+            assert np.array_equal(d.cpu().numpy(), ref), variant
+        finally:
+            eng.set_variant(-1)
 
 
 def test_frag_invalid_and_raw_groups(eng):

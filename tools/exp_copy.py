@@ -30,18 +30,26 @@ def main():
             eng.copy_emit(tx, b, src, cp)
         torch.cuda.synchronize()
     shapes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,3,5").split(",")]
-    for rnd, shape, var in [(r, s, v) for r in range(3) for s in shapes for v in variants]:
+    K = int(os.environ.get("K", "20"))
+    ref = None
+    for rnd, shape, var in [(r, s, v) for r in range(int(os.environ.get("ROUNDS", "3"))) for s in shapes for v in variants]:
         eng.set_shape(shape)
         eng.set_variant(var)
         for _ in range(3):
             eng.copy_emit(tx, b, src, cp)
+        if rnd == 0:  # every (shape, variant) leaves the same bytes
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = tx.clone()
+            elif not torch.equal(ref, tx):
+                raise SystemExit(f"shape {shape} variant {var}: copy-emit output differs from the first one's")
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        for _ in range(20):
+        for _ in range(K):
             eng.copy_emit(tx, b, src, cp)
         z.record()
         torch.cuda.synchronize()
-        ms = a.elapsed_time(z) / 20
+        ms = a.elapsed_time(z) / K
         moved = n * (28 + 1472 + 1472 + 4)
         print(json.dumps({"round": rnd, "shape": shape, "variant": var, "ms": round(ms, 4), "GBs_rw": round(moved / ms / 1e6, 1)}), flush=True)
 
