@@ -97,18 +97,18 @@ int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc
 
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
-    if (variant == 19 || variant == 23 || variant == 24 || variant == 25) return 5;
-    if (variant == 26 || variant == 27) return 13;
+    if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29) return 5;
+    if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
 
 bool line_grid(int variant) {
     return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 19 ||
-           (variant >= 23 && variant <= 27);
+           (variant >= 23 && variant <= 29);
 }
 
 int auto_shape(uint32_t len, bool has_desc, bool line = false, int variant = -1) {
-    if (has_desc) return (variant == 13 || variant == 26 || variant == 27) ? CFG_G16U4 : CFG_G16U3;
+    if (has_desc) return (variant == 13 || variant == 26 || variant == 27 || variant == 28) ? CFG_G16U4 : CFG_G16U3;
     const uint64_t need = (uint64_t)len + (line ? 127 : 15);  // bytes of aligned chunks a record can touch
     // eight records per wavefront in two steps, with as few idle lanes as possible (C4's 1320-B
     // records on the line grid: 8 x 6 0.2083 ms, 8 x 7 0.2188 ms; C2's 1500 B: 8 x 7 0.2327 ms)
@@ -397,7 +397,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 27) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 29) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

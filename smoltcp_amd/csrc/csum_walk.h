@@ -61,23 +61,28 @@ namespace smolcsum {
 template <int VAR>
 struct VarT {
     static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                               (VAR >= 23 && VAR <= 27);
-    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 26 && VAR != 27;
+                               (VAR >= 23 && VAR <= 29);
+    static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 26 && VAR != 27 &&
+                               VAR != 28;
     static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                                 (VAR >= 23 && VAR <= 27);
+                                 (VAR >= 23 && VAR <= 29);
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
     static constexpr bool SHUF2 = VAR == 16;
-    static constexpr bool SEGW = VAR == 19;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
+    static constexpr bool SEGW = VAR == 19 || VAR == 29;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
+    // 29 = 19 with the segment machinery skipped on wavefronts that hold no IPv4 record (a ballot after
+    // the parse: IPv6 records have one field and keep the 2-B store)
+    static constexpr bool SEGW_BALLOT = VAR == 29;
     // 23-27 (emit): whole 64-B field segments with the neighbours' record extents published too, so
     // that they serve descriptor batches as well as fixed strides (SEGG); SEGB: the neighbours of the
     // whole workgroup, not only of the wavefront (a workgroup barrier after the parse, natural grid);
     // SEG6: IPv6 records too.  23 = 5 + SEGG + SEGB + SEG6, 24 = 23 without SEGB, 25 = 23 without
-    // SEG6, 26 = 13 (no prefetch) + SEGG + SEGB + SEG6, 27 = 26 without SEGB.
-    static constexpr bool SEGG = VAR >= 23 && VAR <= 27;
+    // SEG6, 26 = 13 (no prefetch) + SEGG + SEGB + SEG6, 27 = 26 without SEGB, 28 = 27 compiled for
+    // variant 13's occupancy (MinWaves).
+    static constexpr bool SEGG = VAR >= 23 && VAR <= 28;
     static constexpr bool SEGB = VAR == 23 || VAR == 25 || VAR == 26;
-    static constexpr bool SEG6 = VAR == 23 || VAR == 24 || VAR == 26 || VAR == 27;
+    static constexpr bool SEG6 = VAR == 23 || VAR == 24 || VAR == 26 || VAR == 27 || VAR == 28;
 };
 
 template <bool LINE>
@@ -367,10 +372,15 @@ struct SegInfo {
 // SEGG: the same with the record's extent, so that a neighbour can tell whether the bytes of a
 // segment outside its own record belong to this record (descriptor batches: records anywhere).
 // All addresses absolute; [flo, fhi) = the fields' byte range (flo = ~0, fhi = 0: none).
+// Record start `beg` (absolute), length, and [flo, fhi) relative to beg (flo = NO_FIELD, fhi = 0:
+// none).  The group's own decision (record-relative segment starts, SEG_NONE: none) rides in the
+// same entry, so that it costs no registers across the walk.
 struct SegInfoG {
-    uint32_t tag, pad;
-    uint64_t beg, end;
-    uint64_t flo, fhi;
+    uint32_t tag;
+    int32_t segA, segB;
+    uint32_t len;
+    uint64_t beg;
+    uint32_t flo, fhi;
 };
 
 // The record offsets of the fields emit may write (NO_FIELD: none): a superset of finish_gates'.
@@ -597,7 +607,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
           bool SHUF = false, bool WHOLE = false, bool SHUF2 = false, bool SEGW = false, bool SEGG = false,
-          bool SEGB = false, bool SEG6 = false>
+          bool SEGB = false, bool SEG6 = false, bool SEGW_BALLOT = false>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib, SegInfo* si = nullptr, SegInfoG* sg = nullptr,
@@ -750,7 +760,8 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const Geom& g = GREG ? w.gr : *w.g;
             // the lanes sum [0, span_end): the header part is subtracted at the end
             w.s1 = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? (int)g.span_end : 0;
-            if constexpr (SEGW) {
+            if constexpr (SEGW) w.segA = w.segB = SEG_NONE;
+            if (SEGW && (!SEGW_BALLOT || __any(g.fam == 4))) {
                 // publish every field finish_gates may write (a superset is safe), then decide which
                 // of this record's field segments go out whole (see the finish below)
                 uint32_t f[3], lo = NO_FIELD, hi = 0;
@@ -801,67 +812,6 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                     };
                     if (whole(rA)) w.segA = rA;
                     if (rB != rA && whole(rB)) w.segB = rB;
-                }
-            }
-            if constexpr (SEGG) {
-                // publish the record's extent and every field finish_gates may write (a superset is
-                // safe), then decide which of this record's field segments go out whole
-                uint32_t f[3], lo = NO_FIELD, hi = 0;
-                emit_fields(g, f);
-                for (int j = 0; j < 3; ++j)
-                    if (f[j] != NO_FIELD) {
-                        lo = f[j] < lo ? f[j] : lo;
-                        hi = f[j] + 2 > hi ? f[j] + 2 : hi;
-                    }
-                const uint64_t a0 = w.cur.a0, a1 = w.cur.a0 + w.cur.len;
-                if (lane == 0) {
-                    SegInfoG e;
-                    e.tag = (uint32_t)w.r;
-                    e.pad = 0;
-                    e.beg = a0;
-                    e.end = a1;
-                    e.flo = lo != NO_FIELD ? a0 + lo : ~0ull;
-                    e.fhi = lo != NO_FIELD ? a0 + hi : 0ull;
-                    sg[gib] = e;
-                }
-                // SEGB: every group of the workgroup is on its first (and only) record here, so one
-                // barrier makes every neighbour's entry visible (blockwide is uniform over the
-                // workgroup: a natural grid and a full workgroup, see csum_kernel)
-                if (SEGB && blockwide) __syncthreads();
-                else wave_lds_sync();
-                w.segA = w.segB = SEG_NONE;
-                const bool fam_ok = g.fam == 4 || (SEG6 && g.fam == 6);
-                if (fam_ok && lo != NO_FIELD && p.n < 0xFFFFFFFFull && w.cur.len < (1u << 29)) {
-                    constexpr int GPW = 64 / G;
-                    const uint64_t r = w.r;
-                    const bool have_prev = (SEGB && blockwide) ? gib > 0 : (gib % GPW) != 0;
-                    const bool have_next = (SEGB && blockwide) ? gib + 1 < 256 / G : (gib % GPW) != GPW - 1;
-                    // the previous record's extent and last field byte, the next one's (valid only
-                    // when its group holds record r -/+ 1 right now: the tag check)
-                    bool pv = false, nv = false;
-                    uint64_t pbeg = 0, pfhi = 0, nend = 0, nflo = 0;
-                    if (have_prev && r > 0) {
-                        const SegInfoG q = sg[gib - 1];
-                        pv = q.tag == (uint32_t)(r - 1) && q.end == a0;
-                        pbeg = q.beg;
-                        pfhi = q.fhi;
-                    }
-                    if (have_next && r + 1 < p.n) {
-                        const SegInfoG q = sg[gib + 1];
-                        nv = q.tag == (uint32_t)(r + 1) && q.beg == a1;
-                        nend = q.end;
-                        nflo = q.flo;
-                    }
-                    const uint64_t SA = (a0 + lo) & ~63ull, SB = (a0 + hi - 1) & ~63ull;
-                    // the window holds the record's chunks only (past its last one: the dummy line)
-                    const uint64_t wend = base + 16ull * (w.nch < (uint32_t)WIN_CH ? w.nch : (uint32_t)WIN_CH);
-                    auto whole = [&](uint64_t S) {
-                        return SB <= SA + 64 && S + 64 <= wend &&
-                               (S >= a0 || (pv && pbeg <= S && pfhi <= S)) &&
-                               (S + 64 <= a1 || (nv && nend >= S + 64 && nflo >= S + 64));
-                    };
-                    if (whole(SA)) w.segA = (int32_t)(int64_t)(SA - a0);
-                    if (SB != SA && whole(SB)) w.segB = (int32_t)(int64_t)(SB - a0);
                 }
             }
         }
@@ -949,6 +899,87 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
         }
     }
 
+    if constexpr (SEGG) {
+        if (w.step == 0) {
+            // After step 0's sum (fewer registers live than at the parse): publish the record's
+            // extent and every field finish_gates may write (a superset is safe), then decide which
+            // of this record's field segments go out whole.
+            const Geom& g = GREG ? w.gr : *w.g;
+            const uint64_t a0 = w.cur.a0;
+            const int32_t len = (int32_t)w.cur.len;
+            uint32_t lo = NO_FIELD, hi = 0;
+            {
+                uint32_t f[3];
+                emit_fields(g, f);
+                for (int j = 0; j < 3; ++j)
+                    if (f[j] != NO_FIELD) {
+                        lo = f[j] < lo ? f[j] : lo;
+                        hi = f[j] + 2 > hi ? f[j] + 2 : hi;
+                    }
+            }
+            if (lane == 0) {
+                SegInfoG& e = sg[gib];
+                e.tag = (uint32_t)w.r;
+                e.segA = e.segB = SEG_NONE;
+                e.len = w.cur.len;
+                e.beg = a0;
+                e.flo = lo;
+                e.fhi = hi;
+            }
+            // SEGB: every group of the workgroup is on its first (and only) record here, so one
+            // barrier makes every neighbour's entry visible (blockwide is uniform over the
+            // workgroup: a natural grid and a full workgroup, see csum_kernel)
+            if (SEGB && blockwide) __syncthreads();
+            else wave_lds_sync();
+            const bool fam_ok = g.fam == 4 || (SEG6 && g.fam == 6);
+            if (fam_ok && lo != NO_FIELD && p.n < 0xFFFFFFFFull && w.cur.len < (1u << 29)) {
+                constexpr int GPW = 64 / G;
+                const uint64_t r = w.r;
+                const bool have_prev = (SEGB && blockwide) ? gib > 0 : (gib % GPW) != 0;
+                const bool have_next = (SEGB && blockwide) ? gib + 1 < 256 / G : (gib % GPW) != GPW - 1;
+                // Everything relative to this record's start (int32: records are < 2^29 bytes).
+                // The previous record ends here and its last field byte is before pfhi; the next one
+                // starts at len and ends at nend, its first field byte at nflo (valid only when the
+                // neighbour's group holds record r -/+ 1 right now: the tag check, and adjacent in
+                // memory: the extent check)
+                int32_t pbeg = 1 << 30, pfhi = 1 << 30, nend = -(1 << 30), nflo = -(1 << 30);
+                if (have_prev && r > 0) {
+                    const SegInfoG& q = sg[gib - 1];
+                    const uint32_t ql = q.len < (1u << 29) ? q.len : (1u << 29);
+                    if (q.tag == (uint32_t)(r - 1) && q.beg + q.len == a0) {
+                        pbeg = -(int32_t)ql;
+                        pfhi = q.fhi ? (int32_t)q.fhi - (int32_t)ql : pbeg;
+                    }
+                }
+                if (have_next && r + 1 < p.n) {
+                    const SegInfoG& q = sg[gib + 1];
+                    const uint32_t ql = q.len < (1u << 29) ? q.len : (1u << 29);
+                    if (q.tag == (uint32_t)(r + 1) && q.beg == a0 + (uint64_t)len) {
+                        nend = len + (int32_t)ql;
+                        nflo = q.flo != NO_FIELD ? len + (int32_t)q.flo : nend;
+                    }
+                }
+                // record-relative starts of the segments holding the first and the last field byte
+                const int32_t ph = (int32_t)(a0 & 63u);
+                const int32_t SA = ((ph + (int32_t)lo) & ~63) - ph, SB = ((ph + (int32_t)hi - 1) & ~63) - ph;
+                // the window holds the record's chunks only (past its last one: the dummy line)
+                const int32_t head0 = (int32_t)(a0 & (Grid<LINE>::ALIGN - 1));
+                const int32_t wend = 16 * (int32_t)(w.nch < (uint32_t)WIN_CH ? w.nch : (uint32_t)WIN_CH) - head0;
+                auto whole = [&](int32_t S) {
+                    return SB <= SA + 64 && S + 64 <= wend && (S >= 0 || (pbeg <= S && pfhi <= S)) &&
+                           (S + 64 <= len || (nend >= S + 64 && nflo >= S + 64));
+                };
+                const int32_t sa = whole(SA) ? SA : SEG_NONE;
+                const int32_t sb = (SB != SA && whole(SB)) ? SB : SEG_NONE;
+                if (lane == 0) {
+                    sg[gib].segA = sa;
+                    sg[gib].segB = sb;
+                }
+            }
+            wave_lds_sync();  // the decision, read back at the finish
+        }
+    }
+
     if (last) {
         const bool odd = (w.cur.a0 & 1u) != 0;
         const uint64_t r = w.r;
@@ -967,9 +998,14 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             // records and the window holds all of it.  Fields outside such segments are stored as
             // 2-B fields.
             uint64_t wsA = ~0ull, wsB = ~0ull;
-            if constexpr (SEGW || SEGG) {  // the segments decided after the parse (step 0)
+            if constexpr (SEGW) {  // the segments decided after the parse (step 0)
                 if (w.segA != SEG_NONE) wsA = w.cur.a0 + (int64_t)w.segA;
                 if (w.segB != SEG_NONE) wsB = w.cur.a0 + (int64_t)w.segB;
+            }
+            if constexpr (SEGG) {  // the segments decided after step 0's sum
+                const int32_t sa = sg[gib].segA, sb = sg[gib].segB;
+                if (sa != SEG_NONE) wsA = w.cur.a0 + (int64_t)sa;
+                if (sb != SEG_NONE) wsB = w.cur.a0 + (int64_t)sb;
             }
             finish_gates<G, MODE, NHC, decltype(rd), ((COPY && WHOLE) || SEGW || SEGG) ? WIN : 0, SEGW || SEGG>(
                 p, GREG ? w.gr : *w.g, w.acc, rd, winb, head, w.cur.a0, r, lane, reinterpret_cast<uint8_t*>(win),
@@ -1029,8 +1065,15 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 
 // MODE_DATA: checksum::data over [0, len).  MODE_EMIT / MODE_VERIFY: the protocol gates.
 // MODE_COPY: payload copy + emit in one pass.  VAR: see VarT.
+// Occupancy floor (waves per SIMD): variant 28 is 27 held to 7 waves, the occupancy of variant 13 at
+// 16 x 4 (descriptor batches); the segment decision's registers otherwise cost it two waves.
+template <int VAR, int MODE>
+struct MinWaves {
+    static constexpr int value = (MODE == MODE_EMIT && VAR == 28) ? 7 : 1;
+};
+
 template <int G, int U, int MODE, bool IMPLICIT, int VAR, bool NHC = false>
-__global__ __launch_bounds__(256) void csum_kernel(KParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MinWaves<VAR, MODE>::value))) void csum_kernel(KParams p) {
     constexpr bool NT = VarT<VAR>::NT;
     constexpr bool PF = VarT<VAR>::PF;
     constexpr bool LINE = VarT<VAR>::LINE;
@@ -1092,10 +1135,10 @@ __global__ __launch_bounds__(256) void csum_kernel(KParams p) {
                                                   shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6>(
-                    p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6>(
-                    p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6,
+                           VarT<VAR>::SEGW_BALLOT>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6,
+                           VarT<VAR>::SEGW_BALLOT>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
         }
     } else {
         while (true) {
@@ -1161,18 +1204,23 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
         case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
         case 19: return launch_shape<MODE, IMPLICIT, 19>(shape, p, max_blocks, s);
+        case 29:
+            if constexpr (MODE == MODE_EMIT && IMPLICIT) return launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s);
+            return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 23:
         case 24:
         case 25:
         case 26:
         case 27:
+        case 28:
             if constexpr (MODE == MODE_EMIT) {
                 switch (var) {
                     case 23: return launch_seg_shape<IMPLICIT, 23>(shape, p, max_blocks, s);
                     case 24: return launch_seg_shape<IMPLICIT, 24>(shape, p, max_blocks, s);
                     case 25: return launch_seg_shape<IMPLICIT, 25>(shape, p, max_blocks, s);
                     case 26: return launch_seg_shape<IMPLICIT, 26>(shape, p, max_blocks, s);
-                    default: return launch_seg_shape<IMPLICIT, 27>(shape, p, max_blocks, s);
+                    case 27: return launch_seg_shape<IMPLICIT, 27>(shape, p, max_blocks, s);
+                    default: return launch_seg_shape<IMPLICIT, 28>(shape, p, max_blocks, s);
                 }
             }
             return var >= 26 ? launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s)
@@ -1195,7 +1243,7 @@ template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
     // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
-    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 27)) {
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 29)) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);

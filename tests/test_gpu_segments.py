@@ -27,7 +27,7 @@ pytestmark = pytest.mark.gpu
 
 from smoltcp_amd import engine as E  # noqa: E402
 
-SEG_VARIANTS = (23, 24, 25, 26, 27)
+SEG_VARIANTS = (23, 24, 25, 26, 27, 28)
 SHAPES = [0, 1, 2, 3, 4, 5, 6, 7, 8]
 V4A, V4B = bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2])
 A6, B6 = bytes(range(16)), bytes(range(16, 32))
@@ -119,7 +119,7 @@ def test_desc_every_shape(eng):
     rng = np.random.default_rng(3)
     recs = [_record(rng, i, 64, 700) for i in range(700)]
     host, offs, lens = _layout(recs, np.arange(len(recs)), np.zeros(len(recs), int), rng, pad=5)
-    _desc_case(eng, host, offs, lens, E.KIND_IP, variants=(23, 26), blocks_list=(0, 3), shapes=SHAPES)
+    _desc_case(eng, host, offs, lens, E.KIND_IP, variants=(23, 26, 28), blocks_list=(0, 3), shapes=SHAPES)
 
 
 def test_desc_shuffled_and_gapped(eng):
@@ -226,7 +226,8 @@ def test_emit_write_set_concurrent(eng, gap):
     oracle.batch_emit(ref, None, n, stride, L, E.KIND_IP)
     s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
     K = 120
-    for variant, batch in ((19, fixed), (-1, fixed), (23, fixed), (26, desc_batch), (-1, desc_batch)):
+    for variant, batch in ((19, fixed), (29, fixed), (-1, fixed), (23, fixed), (26, desc_batch), (28, desc_batch),
+                           (-1, desc_batch)):
         d = torch.from_numpy(host0.copy()).cuda()
         torch.cuda.synchronize()
         eng.set_variant(variant)
@@ -259,7 +260,7 @@ def test_field_stores_flag(eng):
     ref = host.copy()
     oracle.batch_emit(ref, desc, n)
     batch = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0", batch_flags=E.BATCH_FIELD_STORES)
-    for variant in (-1, 19, 23, 26, 27, 7):
+    for variant in (-1, 19, 23, 26, 27, 28, 29, 7):
         d = torch.from_numpy(host.copy()).cuda()
         eng.set_variant(variant)
         try:
