@@ -89,8 +89,10 @@ constexpr uint32_t kNaturalGrid = 0x7fffffffu;
 // vs 0.2519 ms without).
 int walk_variant(int mode, bool has_desc) {
     // fixed-stride emit: variant 5 with the fields' 64-B segments written whole where no neighbour's
-    // field shares them (C2 emit 0.305 -> 0.294 ms, tools/exp_emit_seg.py)
-    if (!has_desc) return mode == MODE_EMIT ? 19 : 5;
+    // field shares them (C2 emit 0.305 -> 0.294 ms, tools/exp_emit_seg.py), skipped on wavefronts
+    // without an IPv4 record (variant 29: C2 0.2891-0.2894 vs 19's 0.2907-0.2913 ms, C4 0.2649-0.2658
+    // vs 0.2654-0.2666 ms, interleaved on one box, profiles/r04_experiments/)
+    if (!has_desc) return mode == MODE_EMIT ? 29 : 5;
     return mode == MODE_EMIT ? 1 : mode == MODE_VERIFY ? 13 : 5;
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
@@ -181,8 +183,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         // chunks): C2copy 0.772-0.853 ms (variant 16) -> 0.689 ms (tools/exp_copy.py, MI355X).
         // Variants 1 / 8 / 11 / 16 stay selectable.
         const int cv = ctx->variant;
-        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 20) ? cv : 17;
-        const int cshape = ctx->shape >= 0 ? ctx->shape : ((var == 17 || var == 20) ? (int)CFG_G16U4 : shape);
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? cv : 17;
+        const int cshape = ctx->shape >= 0 ? ctx->shape : (var == 17 ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
@@ -455,7 +457,7 @@ const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int h
     if (!ctx || op < MODE_DATA || op > MODE_COPY) return "";
     if (op == MODE_COPY) {
         const int cv = ctx->variant;
-        return (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? "csum_kernel" : cv == 20 ? "copy_tile_kernel" : "copy_kernel";
+        return (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? "csum_kernel" : "copy_kernel";
     }
     const int v = ctx->variant >= 0 ? ctx->variant : auto_variant(op, has_desc != 0);
     const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY);

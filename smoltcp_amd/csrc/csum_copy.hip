@@ -307,408 +307,6 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Copy-emit, third design (variant 20): the tile split of csum_tile.hip applied to copy_kernel.
-//
-// A wavefront owns a TILE of T consecutive records and works on it in four phases:
-//   A  lane i reads record i's descriptor and copy descriptor into LDS;
-//   B  each group of G lanes copies and sums its records one after the other, exactly as
-//      copy_kernel does (round 1: the 128-B window, the generic chunks past it and the first UB * G
-//      body chunks; then body rounds of U * G chunks), but without any parse: it sums the record's
-//      whole buffer [0, len), stores every chunk past the window, and leaves the window (with the
-//      payload merged in) in the record's LDS row;
-//   C  lane i parses record i from its row, takes the bytes outside the L4 span back out of the
-//      sum, applies the gates and patches the fields into the row (a field past the window goes
-//      to global memory after the wave's chunk stores have completed);
-//   D  the groups store the window chunks from the rows.
-// Parse and gates run once per lane for 64 records per instruction, instead of redundantly on the
-// G lanes of each record's group (copy_kernel: ~12 % of its time).
-// ---------------------------------------------------------------------------------------------
-namespace ctile {
-
-constexpr int WROW = 33;  // dwords per window row: 128 B + 4 (odd: phase C's lane-per-row reads
-                          // hit distinct banks)
-
-template <int T>
-struct Lds {
-    uint32_t win[T * WROW];
-    uint32_t sum[T];
-    uint32_t info[T * 8];  // a0 lo / hi, len, kind (| KIND_BAD_COPY), sb lo / hi, p0, p1
-};
-
-__device__ __forceinline__ uint32_t rbyte(const uint32_t* row, uint32_t x) {
-    return (row[x >> 2] >> (8 * (x & 3))) & 0xffu;
-}
-
-// Aligned-word contribution of window bytes [from, to), to <= WIN.
-__device__ __forceinline__ uint32_t row_sum(const uint32_t* row, uint32_t from, uint32_t to) {
-    uint32_t acc = 0;
-    for (uint32_t d = from >> 2; d < ((to + 3) >> 2); ++d) {
-        const int lo = (int)from - (int)(4 * d), hi = (int)to - (int)(4 * d);
-        acc = add_words(mask_dword(row[d], lo, hi), acc);
-    }
-    return acc;
-}
-
-}  // namespace ctile
-
-template <int G, int U, bool IMPLICIT, int UB, int T>
-__global__ __launch_bounds__(256) void copy_tile_kernel(KParams p) {
-    using namespace copy2;
-    using namespace ctile;
-    constexpr int GPW = 64 / G;
-    constexpr int UW = 1;                                   // round-1 generic slots per lane
-    constexpr uint32_t NEX = (uint32_t)(UW * G - WIN_CH);  // of which past the window
-    static_assert(G == 16 || G == 32, "group size");
-    static_assert(T % GPW == 0 && T <= 64, "tile");
-    __shared__ Lds<T> lds[4];
-    const int wave = (int)(threadIdx.x >> 6);
-    const int lane = (int)(threadIdx.x & 63);
-    const int gl = lane % G;
-    const int grp = lane / G;
-    Lds<T>& L = lds[wave];
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
-    const uint64_t dummy = (uint64_t)p.dummy;
-
-    for (uint64_t tile = (uint64_t)blockIdx.x * 4 + wave; tile * T < p.n; tile += nwaves) {
-        const uint64_t r0 = tile * T;
-        const uint32_t cnt = (uint32_t)((p.n - r0) < (uint64_t)T ? (p.n - r0) : (uint64_t)T);
-
-        // ---- phase A: lane i's record and copy range ----
-        if (lane < T) {
-            const uint64_t r = r0 + ((uint32_t)lane < cnt ? (uint32_t)lane : 0u);
-            const RecRef rr = rec_at<IMPLICIT, true>(p, r);
-            uint32_t* in = &L.info[8 * lane];
-            in[0] = (uint32_t)rr.a0;
-            in[1] = (uint32_t)(rr.a0 >> 32);
-            in[2] = (uint32_t)lane < cnt ? rr.len : 0u;
-            in[3] = rr.kind;
-            in[4] = (uint32_t)rr.sb;
-            in[5] = (uint32_t)(rr.sb >> 32);
-            in[6] = rr.p0;
-            in[7] = rr.p1;
-        }
-        wave_lds_sync();
-        auto rec = [&](int q) -> RecRef {
-            const uint32_t* in = &L.info[8 * q];
-            RecRef rr;
-            rr.a0 = (uint64_t)in[0] | ((uint64_t)in[1] << 32);
-            rr.len = in[2];
-            rr.kind = in[3];
-            rr.sb = (uint64_t)in[4] | ((uint64_t)in[5] << 32);
-            rr.p0 = in[6];
-            rr.p1 = in[7];
-            return rr;
-        };
-
-        // ---- phase B: copy + sum, each group over its records ----
-        for (int j = 0; j < T / GPW; ++j) {
-            const int q = j * GPW + grp;
-            const RecRef rr = rec(q);
-            if (rr.len == 0 || (rr.kind & KIND_BAD_COPY)) {  // past the batch / left untouched
-                if (gl == 0) L.sum[q] = 0;
-                continue;
-            }
-            uint32_t* row = &L.win[q * WROW];
-            const uint64_t base = rr.a0 & ~15ull;
-            const uint32_t head = (uint32_t)(rr.a0 - base);
-            const uint32_t nch = n_chunks<false>(rr);
-            const bool pay = rr.p1 > rr.p0;
-            const uint64_t sk = rr.sb - head;
-            const uint64_t first = (rr.sb + rr.p0) & ~15ull, last = (rr.sb + rr.p1 - 1) & ~15ull;
-            uint32_t kb0 = pay ? (head + rr.p0 + 15) >> 4 : nch;
-            kb0 = kb0 > (uint32_t)WIN_CH ? kb0 : (uint32_t)WIN_CH;
-            uint32_t kb1 = pay ? (head + rr.p1) >> 4 : 0u;
-            kb1 = kb1 < nch ? kb1 : nch;
-            kb1 = kb1 > kb0 ? kb1 : kb0;
-            const uint32_t e1 = kb0 < nch ? kb0 : nch;
-            const uint32_t n1 = e1 > (uint32_t)WIN_CH ? e1 - WIN_CH : 0u;
-            const uint32_t n2 = nch > kb1 ? nch - kb1 : 0u;
-            const uint32_t ne = n1 + n2;
-            auto gen_k = [&](uint32_t e) -> uint32_t { return e < n1 ? WIN_CH + e : kb1 + (e - n1); };
-            const uint32_t nb = kb1 - kb0;
-            const uint32_t nbe = nb < (uint32_t)(UB * G) ? nb : (uint32_t)(UB * G);
-            auto gen_load = [&](uint32_t k, bool in, u32x4& d, u32x4& c0, u32x4& c1) {
-                const int pos = (int)(16u * k) - (int)head;
-                const int lo = (int)rr.p0 - pos, hi = (int)rr.p1 - pos;
-                const bool full = lo <= 0 && hi >= 16;
-                const bool any = pay && lo < 16 && hi > 0;
-                d = ld16<false>((gcv4)(in && !(pay && full) ? base + 16ull * k : dummy));
-                const uint64_t sA = (sk + 16ull * k) & ~15ull;
-                const uint64_t a0 = sA < first ? first : sA > last ? last : sA;
-                const uint64_t a1 = sA + 16 < first ? first : sA + 16 > last ? last : sA + 16;
-                c0 = ld16<false>((gcv4)(in && any ? a0 : dummy));
-                c1 = ld16<false>((gcv4)(in && any && (sk & 15u) ? a1 : dummy));
-            };
-            auto gen_merge = [&](uint32_t k, const u32x4& d, const u32x4& c0, const u32x4& c1) -> u32x4 {
-                const int pos = (int)(16u * k) - (int)head;
-                const int lo = (int)rr.p0 - pos, hi = (int)rr.p1 - pos;
-                if (!(pay && lo < 16 && hi > 0)) return d;
-                const u32x4 s = funnel16(c0, c1, (uint32_t)(sk & 15u));
-                if (lo <= 0 && hi >= 16) return s;
-                u32x4 m;
-                const uint32_t m0 = byte_mask(lo, hi, 0), m1 = byte_mask(lo, hi, 1);
-                const uint32_t m2 = byte_mask(lo, hi, 2), m3 = byte_mask(lo, hi, 3);
-                m.x = (s.x & m0) | (d.x & ~m0);
-                m.y = (s.y & m1) | (d.y & ~m1);
-                m.z = (s.z & m2) | (d.z & ~m2);
-                m.w = (s.w & m3) | (d.w & ~m3);
-                return m;
-            };
-            const uint64_t skA = sk & ~3ull;
-            const uint32_t b = (uint32_t)(sk & 3u);
-            const bool need_hi = __any(b != 0u);
-            const int len = (int)rr.len;
-            uint32_t acc = 0;
-            // round 1: the window, the first generic chunks past it, the first body chunks
-            u32x4 elo[UB];
-            uint32_t ehi[UB];
-            {
-                u32x4 d, c0, c1;
-                const uint32_t jj = (uint32_t)gl;
-                const bool w = jj < (uint32_t)WIN_CH;
-                const uint32_t k = w ? jj : gen_k(jj - WIN_CH);
-                const bool in = w ? jj < nch : jj - WIN_CH < ne;
-                gen_load(k, in, d, c0, c1);
-#pragma unroll
-                for (int u = 0; u < UB; ++u) {
-                    const uint32_t i = (uint32_t)(u * G + gl);
-                    const uint64_t A = skA + 16ull * (kb0 + i);
-                    elo[u] = ld16<false>((gcv4)(i < nb ? A : dummy));
-                    ehi[u] = need_hi ? *(const GMEM uint32_t*)(i < nb && b ? A + 16 : dummy) : 0u;
-                }
-                const u32x4 m = gen_merge(k, d, c0, c1);
-                if (in) {
-                    const int pos = (int)(16u * k) - (int)head;
-                    acc = sum_chunk(m, pos, len, acc);
-                    if (w) {
-                        row[4 * k] = m.x;
-                        row[4 * k + 1] = m.y;
-                        row[4 * k + 2] = m.z;
-                        row[4 * k + 3] = m.w;
-                    } else {
-                        store_part((gu8)base + 16u * k, m, -pos, len - pos, NOF, NOF, NOF);
-                    }
-                }
-            }
-            // generic chunks beyond round 1
-            for (uint32_t e0 = NEX; e0 < ne; e0 += G) {
-                const uint32_t e = e0 + (uint32_t)gl;
-                const bool in = e < ne;
-                const uint32_t k = gen_k(in ? e : 0u);
-                u32x4 d, c0, c1;
-                gen_load(k, in, d, c0, c1);
-                const u32x4 m = gen_merge(k, d, c0, c1);
-                if (in) {
-                    const int pos = (int)(16u * k) - (int)head;
-                    acc = sum_chunk(m, pos, len, acc);
-                    store_part((gu8)base + 16u * k, m, -pos, len - pos, NOF, NOF, NOF);
-                }
-            }
-            // body: copy + sum
-            auto body_proc = [&](uint32_t i, const u32x4& lo, uint32_t hi) {
-                const uint32_t k = kb0 + i;
-                u32x4 m;
-                m.x = __builtin_amdgcn_alignbyte(lo.y, lo.x, b);
-                m.y = __builtin_amdgcn_alignbyte(lo.z, lo.y, b);
-                m.z = __builtin_amdgcn_alignbyte(lo.w, lo.z, b);
-                m.w = __builtin_amdgcn_alignbyte(hi, lo.w, b);
-                const int pos = (int)(16u * k) - (int)head;
-                acc = sum_chunk(m, pos, len, acc);
-                *(GMEM u32x4*)((gu8)base + 16u * k) = m;
-            };
-#pragma unroll
-            for (int u = 0; u < UB; ++u) {
-                const uint32_t i = (uint32_t)(u * G + gl);
-                if (i < nbe) body_proc(i, elo[u], ehi[u]);
-            }
-            for (uint32_t i0 = nbe; i0 < nb; i0 += (uint32_t)(G * U)) {
-                u32x4 blo[U];
-                uint32_t bhi[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t i = i0 + (uint32_t)(u * G + gl);
-                    const uint64_t A = skA + 16ull * (kb0 + i);
-                    blo[u] = ld16<false>((gcv4)(i < nb ? A : dummy));
-                    bhi[u] = need_hi ? *(const GMEM uint32_t*)(i < nb && b ? A + 16 : dummy) : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t i = i0 + (uint32_t)(u * G + gl);
-                    if (i < nb) body_proc(i, blo[u], bhi[u]);
-                }
-            }
-            const uint32_t tot = group_sum<G>(acc);
-            if (gl == 0) L.sum[q] = tot;
-        }
-        wave_lds_sync();
-
-        // ---- phase C: lane i finishes record i ----
-        bool far = false;
-        uint32_t far_a = 0, far_b = 0, far_c = 0;  // record offsets of fields past the window (+1; 0: none)
-        uint32_t far_va = 0, far_vb = 0, far_vc = 0;
-        if ((uint32_t)lane < cnt) {
-            const RecRef rr = rec(lane);
-            const uint64_t r = r0 + lane;
-            if (rr.kind & KIND_BAD_COPY) {
-                if (p.status) ((gu8)p.status)[r] = (uint8_t)SMOL_ST_MALFORMED;
-            } else {
-                uint32_t* row = &L.win[lane * WROW];
-                uint8_t* rowb = reinterpret_cast<uint8_t*>(row);
-                const uint32_t head = (uint32_t)(rr.a0 & 15u);
-                const uint32_t nch = n_chunks<false>(rr);
-                const uint32_t wvalid = nch * 16 < (uint32_t)WIN ? nch * 16 : (uint32_t)WIN;
-                const bool odd = (rr.a0 & 1u) != 0;
-                // record byte o (o < len): the row, else global memory (payload bytes from the source;
-                // the others are unchanged by this kernel, fields included until phase C writes them)
-                auto rd = [&](uint32_t o) -> uint32_t {
-                    const uint32_t x = head + o;
-                    if (x < wvalid) return rbyte(row, x);
-                    if (o >= rr.p0 && o < rr.p1) return ld_byte_sync(rr.sb + o);
-                    return ld_byte_sync(rr.a0 + o);
-                };
-                auto rsum = [&](uint32_t from, uint32_t to) -> uint32_t {  // record offsets
-                    if (head + to <= wvalid) return row_sum(row, head + from, head + to);
-                    uint32_t a = 0;
-                    for (uint32_t o = from; o < to; ++o) a += rd(o) << (8 * ((head + o) & 1));
-                    return a;
-                };
-                const Geom g = parse_geometry<false>(rd, rr.len, rr.kind, true);
-                const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
-                uint32_t fip = MF_NONE, fl4 = MF_NONE, fin = MF_NONE, vip = 0, vl4 = 0, vin = 0;
-                auto word = [&](uint32_t v) { return odd ? v : bswap16(v); };  // BE u16 at an even offset
-                if (g.fam == 4) {
-                    const uint32_t f0 = rd(g.ip_off + 10), f1 = rd(g.ip_off + 11);
-                    const uint32_t sh = rsum(g.ip_off, g.ip_off + g.ip_hl) - (odd ? ((f0 << 8) + f1) : (f0 + (f1 << 8)));
-                    const uint32_t f = fold32(sh);
-                    const uint32_t hdr = odd ? f : bswap16(f);  // == checksum::data(header)
-                    fip = g.ip_off + 10;
-                    vip = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
-                }
-                if (l4) {
-                    const uint32_t fpos = g.l4_off + g.fo;
-                    const uint32_t field = (rd(fpos) << 8) | rd(fpos + 1);
-                    uint32_t s = L.sum[lane] - rsum(0, g.l4_off);
-                    if (g.span_end < rr.len) s -= rsum(g.span_end, rr.len);
-                    s -= word(field);
-                    if (g.in_off) {  // ICMPv4 error: the embedded IPv4 header first
-                        uint32_t hin = 0;
-                        for (uint32_t i = 0; i < g.in_hl / 2; ++i)
-                            if (i != 5) hin += (rd(g.in_off + 2 * i) << 8) | rd(g.in_off + 2 * i + 1);
-                        fin = g.in_off + 10;
-                        vin = caps_tx(p.caps_ipv4) ? (~fold32(hin) & 0xffffu) : 0u;
-                        s = s - word((rd(fin) << 8) | rd(fin + 1)) + word(vin);
-                    }
-                    const uint32_t f = fold32(s);
-                    const uint32_t dat = odd ? f : bswap16(f);  // == checksum::data(span)
-                    const bool pseudo = g.proto == P_UDP || g.proto == P_TCP || g.proto == P_ICMP6;
-                    uint32_t ph = 0;
-                    if (pseudo) {
-                        const uint32_t xa = fold32(rsum(g.addr_off, g.addr_off + 2 * g.addr_words));
-                        const uint32_t addr = odd ? xa : bswap16(xa);
-                        const uint32_t plen = g.proto == P_UDP ? (g.span_end - g.l4_off) : g.l4_len;
-                        ph = fold32(addr + g.proto + (plen & 0xffffu));  // pseudo_header()
-                    }
-                    const uint32_t comb = pseudo ? fold32(ph + dat) : dat;  // combine()
-                    uint32_t gate_caps;
-                    switch (g.proto) {
-                        case P_UDP: gate_caps = p.caps_udp; break;
-                        case P_TCP: gate_caps = p.caps_tcp; break;
-                        case P_ICMP4: gate_caps = p.caps_icmpv4; break;
-                        case P_ICMP6: gate_caps = p.caps_icmpv6; break;
-                        default: gate_caps = SMOL_CHECKSUM_NONE; break;  // IGMP
-                    }
-                    const bool fill = g.proto == P_IGMP ? true : caps_tx(gate_caps);
-                    uint32_t c = ~comb & 0xffffu;
-                    if (g.proto == P_UDP && c == 0) c = 0xffffu;  // udp.rs:207
-                    fl4 = fpos;
-                    vl4 = fill ? c : 0u;
-                }
-                // the fields into the row (phase D stores it), or past it: after the chunk stores
-                // (a field across the window's edge: both, so that phase D's store of the window
-                // chunk writes the new byte too)
-                auto put = [&](uint32_t f, uint32_t v, uint32_t& fa, uint32_t& va) {
-                    if (f == MF_NONE) return;
-                    if (head + f < wvalid) rowb[head + f] = (uint8_t)(v >> 8);
-                    if (head + f + 1 < wvalid) rowb[head + f + 1] = (uint8_t)v;
-                    if (head + f + 2 > wvalid) {
-                        far = true;
-                        fa = f + 1;
-                        va = v;
-                    }
-                };
-                put(fip, vip, far_a, far_va);
-                put(fin, vin, far_c, far_vc);
-                put(fl4, vl4, far_b, far_vb);
-                if (p.status) ((gu8)p.status)[r] = (uint8_t)g.st;
-            }
-        }
-        if (__any(far)) {
-            // a field past the window lies in a chunk a group stored in phase B (with its old
-            // value): every store of the wave completes first, then the field goes out
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (far) {
-                const uint64_t a0 = (uint64_t)L.info[8 * lane] | ((uint64_t)L.info[8 * lane + 1] << 32);
-                if (far_a) store_be16((gu8)(a0 + far_a - 1), far_va);
-                if (far_c) store_be16((gu8)(a0 + far_c - 1), far_vc);
-                if (far_b) store_be16((gu8)(a0 + far_b - 1), far_vb);
-            }
-        }
-        wave_lds_sync();
-
-        // ---- phase D: the window chunks, fields patched in ----
-        for (int j = 0; j < T / GPW; ++j) {
-            const int q = j * GPW + grp;
-            const RecRef rr = rec(q);
-            if (rr.len == 0 || (rr.kind & KIND_BAD_COPY)) continue;
-            const uint32_t* row = &L.win[q * WROW];
-            const uint64_t base = rr.a0 & ~15ull;
-            const uint32_t head = (uint32_t)(rr.a0 - base);
-            const uint32_t nch = n_chunks<false>(rr);
-            const uint32_t k = (uint32_t)gl;
-            if (k < (uint32_t)WIN_CH && k < nch) {
-                u32x4 c;
-                c.x = row[4 * k];
-                c.y = row[4 * k + 1];
-                c.z = row[4 * k + 2];
-                c.w = row[4 * k + 3];
-                const int pos = (int)(16u * k) - (int)head;
-                store_part((gu8)base + 16u * k, c, -pos, (int)rr.len - pos, NOF, NOF, NOF);
-            }
-        }
-        wave_lds_sync();  // the rows are rewritten by the next tile
-    }
-}
-
-template <bool IMPLICIT, int G, int U, int UB, int T>
-hipError_t launch_copy_tile_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    const uint64_t tiles = (p.n + T - 1) / T;
-    const uint64_t want = (tiles + 3) / 4;
-    const uint64_t cap = p.num_cu == 0 ? max_blocks : (uint64_t)0x7fffffff;  // explicit cap: persistent
-    const uint32_t blocks = grid_blocks(want, cap);
-    hipLaunchKernelGGL((copy_tile_kernel<G, U, IMPLICIT, UB, T>), dim3(blocks), dim3(256), 0, s, p);
-    return hipGetLastError();
-}
-
-// Shapes: 16 x 4 x 2 body slots in round 1 with 32-record tiles (the default: 84 VGPRs, 5 waves per
-// SIMD; 64-record tiles hold 43 KB of LDS per workgroup, 3 waves per SIMD) or 64-record tiles
-// (CFG_G16U3); 32 x 2 x 1 and 16 x 5 x 1 with 32-record tiles.
-template <bool IMPLICIT>
-hipError_t launch_copy_tile(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    switch (shape) {
-        case CFG_G16U3: return launch_copy_tile_one<IMPLICIT, 16, 4, 2, 64>(p, max_blocks, s);
-        case CFG_G32U3:
-        case CFG_G32U4: return launch_copy_tile_one<IMPLICIT, 32, 2, 1, 32>(p, max_blocks, s);
-        case CFG_G16U6: return launch_copy_tile_one<IMPLICIT, 16, 5, 1, 32>(p, max_blocks, s);
-        default: return launch_copy_tile_one<IMPLICIT, 16, 4, 2, 32>(p, max_blocks, s);
-    }
-}
-
-hipError_t launch_copy_v20(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
-    return p.desc == nullptr ? launch_copy_tile<true>(shape, p, max_blocks, s)
-                             : launch_copy_tile<false>(shape, p, max_blocks, s);
-}
-
 template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0>
 hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;

@@ -293,8 +293,9 @@ __global__ __launch_bounds__(256) void field_probe_kernel(uint8_t* buf, uint64_t
 // The same probe with the store addresses given as a list (descriptor batches, whose fields do not
 // sit at a fixed spacing): addrs[] ascending byte offsets of 2-byte stores, first[j] the index of the
 // first address inside the 8-KiB piece j (first[] has ceil(bytes / 8 KiB) + 1 entries).
-// seg64: rewrite the whole 64-B segment holding each address instead (with the values it holds:
-// loaded by the storing lane, an L2 hit after the piece's stream) — the store shape of variant 19.
+// seg64: instead, the 64-B segments holding each listed field (both of its bytes) are rewritten
+// whole with the values the stream just read: each lane stores those of its 16-B chunks that lie in
+// such a segment, from its registers (no reload) — the store shape of whole-segment emit.
 __global__ __launch_bounds__(256) void field_probe_list_kernel(uint8_t* buf, uint64_t n16, const uint64_t* addrs,
                                                                const uint32_t* first, int seg64) {
     constexpr int UNR = 8;
@@ -304,24 +305,10 @@ __global__ __launch_bounds__(256) void field_probe_list_kernel(uint8_t* buf, uin
     const uint64_t per = 64ull * UNR;
     const uint64_t bytes = n16 * 16;
     const u32x4s* q = reinterpret_cast<const u32x4s*>(buf);
+    typedef __attribute__((address_space(1))) u32x4s* gv4;
     auto stores = [&](uint64_t piece, uint32_t acc) {
         const uint32_t i0 = first[piece], i1 = first[piece + 1];
-        for (uint32_t i = i0 + (uint32_t)lane; i < i1; i += 64) {
-            if (seg64) {
-                const uint64_t a = addrs[i] & ~63ull;
-                if (a + 64 <= bytes) {
-                    typedef __attribute__((address_space(1))) u32x4s* gv4;
-                    const gv4 g = (gv4)(buf + a);
-                    const u32x4s x0 = g[0], x1 = g[1], x2 = g[2], x3 = g[3];
-                    g[0] = x0;
-                    g[1] = x1;
-                    g[2] = x2;
-                    g[3] = x3;
-                }
-            } else {
-                probe_store(buf, bytes, addrs[i], acc + i);
-            }
-        }
+        for (uint32_t i = i0 + (uint32_t)lane; i < i1; i += 64) probe_store(buf, bytes, addrs[i], acc + i);
     };
     for (uint64_t base = w0 * per; base + per <= n16; base += nw * per) {
         u32x4s v[UNR];
@@ -332,13 +319,38 @@ __global__ __launch_bounds__(256) void field_probe_list_kernel(uint8_t* buf, uin
         for (int u = 0; u < UNR; ++u)
             acc += __builtin_amdgcn_sad_u16(v[u].x, 0, 0) + __builtin_amdgcn_sad_u16(v[u].y, 0, 0) +
                    __builtin_amdgcn_sad_u16(v[u].z, 0, 0) + __builtin_amdgcn_sad_u16(v[u].w, 0, 0);
-        stores(base / per, acc);
+        // every piece is read, stores or not: without this the compiler sinks the loads into the
+        // store loop
+        asm volatile("" ::"v"(acc));
+        if (seg64) {
+            const uint64_t piece = base / per;
+            const uint32_t i0 = first[piece], i1 = first[piece + 1];
+            // a segment of this piece holds a field when one of the listed offsets (or the byte after
+            // it) falls in it; the piece's offsets are few (C2: about 11 per 8 KiB)
+            uint32_t hit = 0;  // bit u: chunk u of this lane lies in a field segment
+            for (uint32_t i = i0; i < i1; ++i) {
+                const uint64_t a = addrs[i];
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    const uint64_t sgm = (16ull * (base + u * 64 + lane)) & ~63ull;
+                    if ((a & ~63ull) == sgm || ((a + 1) & ~63ull) == sgm) hit |= 1u << u;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                u32x4s x = v[u];
+                asm volatile("" : "+v"(x));  // opaque: the stored values are the ones just read
+                if (hit & (1u << u)) ((gv4)buf)[base + u * 64 + lane] = x;
+            }
+        } else {
+            stores(base / per, acc);
+        }
     }
     const uint64_t tail = n16 / per * per;
     if (w0 == 0 && tail < n16) {
         uint32_t acc = 0;
         for (uint64_t i = tail + (uint64_t)lane; i < n16; i += 64) acc += q[i].x;
-        stores(tail / per, acc);
+        if (!seg64) stores(tail / per, acc);
     }
 }
 

@@ -136,7 +136,7 @@ def test_raw_records_fixed_stride_and_copy_emit(eng):
     copies = E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472)
     ref = h.copy()
     oracle.batch_copy_emit(ref, None, n, src, copies, L, L, oracle.kind_flags(E.KIND_IP, E.REC_IPHDR_ONLY))
-    for variant in (-1, 17, 20):
+    for variant in (-1, 1, 17):
         eng.set_variant(variant)
         try:
             d = torch.from_numpy(h.copy()).cuda()
