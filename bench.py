@@ -58,6 +58,8 @@ def parse_args(argv=None):
                     help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
     ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
     ap.add_argument("--variant", type=int, default=-1, help="force a kernel variant (tuning)")
+    ap.add_argument("--xcd-remap", type=int, default=-1, help="1/0: force the XCD-contiguous block order (tuning)")
+    ap.add_argument("--launch-records", type=int, default=-1, help="records per kernel launch (tuning; 0: all)")
     ap.add_argument("--probe", action="store_true", help="(kept for old scripts: the probes always run)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch + rendezvous + reporting only, on CPU (gloo), no checksum work")
@@ -584,6 +586,10 @@ def main(argv=None):
         eng.set_shape(args.shape)
     if args.variant >= 0:
         eng.set_variant(args.variant)
+    if args.xcd_remap >= 0:
+        eng.set_xcd_remap(args.xcd_remap)
+    if args.launch_records >= 0:
+        eng.set_launch_records(args.launch_records)
     wl = Workload(E, eng, args.config, args.n, rank, dev)
     torch.cuda.synchronize()
 
@@ -703,6 +709,39 @@ def main(argv=None):
                  "seg64_what": "the same stream with the 64-B segment holding each checksum field rewritten "
                                "whole (its own values): the floor of a whole-segment emit"}
 
+    # Fresh batches (rank 0, batches of at most 4 GB): the timed steps re-emit the same TX batch, and
+    # the ~70 MB of field segments one C2 pass writes stay dirty in the 256-MB Infinity Cache, where
+    # the next pass rewrites them; a TX path that emits a new batch every time pays their DRAM writes
+    # (DESIGN.md §5).  Emit over R = 4 batches in turn beside emit over one, interleaved.
+    fresh = None
+    if rank == 0 and wl.copy is None and wl.tx.numel() <= (4 << 30):
+        R = 4
+        txs = [wl.tx] + [wl.tx.clone() for _ in range(R - 1)]
+        torch.cuda.synchronize()
+
+        def emit_loop(bufs, reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for i in range(R):
+                eng.emit(bufs[i % len(bufs)], wl.batch, stream=stream)
+            a.record(stream)
+            for i in range(reps):
+                eng.emit(bufs[i % len(bufs)], wl.batch, stream=stream)
+            b.record(stream)
+            torch.cuda.synchronize()
+            return a.elapsed_time(b) / reps
+
+        same, rot = [], []
+        for _ in range(3):
+            same.append(emit_loop(txs[:1], 4 * R))
+            rot.append(emit_loop(txs, 4 * R))
+        del txs
+        torch.cuda.empty_cache()
+        fresh = {"emit_same_batch_ms": round(float(np.median(same)), 4),
+                 "emit_fresh_batches_ms": round(float(np.median(rot)), 4), "batches": R,
+                 "what": "emit alone over the same TX batch (as in the timed steps) and over 4 batches in turn "
+                         "(every emit a batch its previous pass did not just write): the second pays the DRAM "
+                         "writes of the field segments that the Infinity Cache absorbs in the first"}
+
     unfused = None
     if wl.copy is not None and rank == 0:
         # the unfused TX path for comparison: payload copy (strided device copy) then emit
@@ -777,6 +816,7 @@ def main(argv=None):
                      "what": "untimed steps before the W warm-up steps until the GPU clocks have ramped "
                              "(steady state: profiles/r03_steps/)"},
             "verify_rejected": rejected,
+            "emit_fresh_batches": fresh,
             "per_rank": per_rank,
             "cpu_baseline": cpu,
             "parity_sample": parity,

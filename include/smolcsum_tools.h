@@ -65,6 +65,15 @@ int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records);
 /* Cap the number of workgroups per launch (0 = automatic: CUs x 8). */
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
 
+/* Walk-kernel launches with on = 1 map workgroup b to the records of workgroup xcd_block(b)
+ * (csum_launch.h): the workgroups that share an XCD take one contiguous range of the batch.  0 (the
+ * default): the natural order. */
+int smol_csum_tool_set_xcd_remap(smol_csum_ctx_t* ctx, int on);
+
+/* Batched calls over more than `records` records (0: no limit, the default) go out as consecutive
+ * kernel launches of at most `records` records each, on the same stream. */
+int smol_csum_tool_set_launch_records(smol_csum_ctx_t* ctx, uint64_t records);
+
 /* Read-only HBM streaming probe over `bytes` (multiple of 16, 16-byte aligned `d_buf`): the
  * achievable read ceiling that the checksum kernels are compared with.  Each wavefront streams
  * contiguous 8-KiB pieces with eight non-temporal 16-byte loads per lane in flight (the fastest

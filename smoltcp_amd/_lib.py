@@ -35,6 +35,7 @@ TOOL_SYMBOLS = [
     "smol_csum_tool_synth", "smol_csum_tool_corrupt", "smol_csum_tool_set_shape",
     "smol_csum_tool_set_variant", "smol_csum_tool_set_tile",
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
+    "smol_csum_tool_set_xcd_remap", "smol_csum_tool_set_launch_records",
     "smol_csum_tool_field_probe",
     "smol_csum_tool_field_probe_list",
     "smol_csum_tool_kernel_name",
@@ -136,6 +137,10 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_tool_set_tile.restype = i32
     L.smol_csum_tool_set_max_blocks.argtypes = [vp, u32]
     L.smol_csum_tool_set_max_blocks.restype = i32
+    L.smol_csum_tool_set_xcd_remap.argtypes = [vp, ctypes.c_int]
+    L.smol_csum_tool_set_xcd_remap.restype = i32
+    L.smol_csum_tool_set_launch_records.argtypes = [vp, u64]
+    L.smol_csum_tool_set_launch_records.restype = i32
     L.smol_csum_tool_stream_read.argtypes = [vp, vp, u64, vp, vp]
     L.smol_csum_tool_stream_read.restype = i32
     L.smol_csum_tool_field_probe.argtypes = [vp, vp, u64, u64, ctypes.c_uint32, ctypes.c_uint32, vp]

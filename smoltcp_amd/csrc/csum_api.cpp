@@ -24,6 +24,8 @@ struct smol_csum_ctx {
     uint8_t* dummy;       // 256 zero bytes on the device (target of loads with nothing to read)
     int tile_records;     // tile kernel: records per wavefront tile (32 or 64)
     bool max_blocks_set;  // grid cap given explicitly (tooling)
+    int xcd_remap;        // walk kernel: each XCD's blocks take a contiguous range of records (tooling)
+    uint64_t launch_records;  // records per kernel launch (0: the whole batch in one launch)
 };
 
 namespace smolcsum {
@@ -162,6 +164,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.status = d_status;
     p.dummy = ctx->dummy;
     p.num_cu = ctx->max_blocks_set ? 0u : (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);
+    p.xcd_remap = (uint32_t)ctx->xcd_remap;
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
     // Variants: 0-2, 5-6 = walk kernel (csum_walk.h VarT: load policy, prefetch, chunk
@@ -177,6 +180,25 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool use_tile = variant == 3 || variant == 4 || variant == 7;
     int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, has_desc, line_grid(variant), variant);
     const hipStream_t s = (hipStream_t)stream;
+    // A batch larger than launch_records records goes out as consecutive launches on the stream,
+    // each over the next launch_records records (the per-record arrays advance with them).
+    const uint64_t per = ctx->launch_records ? ctx->launch_records : b->n;
+    if (per < b->n) {
+        for (uint64_t i0 = 0; i0 < b->n; i0 += per) {
+            smol_csum_batch_t sub = *b;
+            sub.n = b->n - i0 < per ? b->n - i0 : per;
+            uint8_t* buf = d_buf;
+            if (b->desc) sub.desc = b->desc + i0;
+            else buf = d_buf + i0 * b->stride;
+            const uint64_t keep = ctx->launch_records;
+            ctx->launch_records = 0;
+            const int rc = run(ctx, mode, buf, &sub, caps, d_out ? d_out + i0 : nullptr, d_status ? d_status + i0 : nullptr,
+                               stream, d_src, d_copy ? d_copy + i0 : nullptr, d_addrs ? d_addrs + 32 * i0 : nullptr);
+            ctx->launch_records = keep;
+            if (rc != SMOL_OK) return rc;
+        }
+        return SMOL_OK;
+    }
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
         // default: variant 17 (csum_copy.hip: body chunks = one source load + shift + sum + store,
         // window and edge chunks generic) at its default shape (16 x 4, round 1 carrying 32 body
@@ -237,6 +259,8 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     c->dummy = dummy;
     c->tile_records = 32;
     c->max_blocks_set = false;
+    c->xcd_remap = 0;
+    c->launch_records = 0;
     c->device = device;
     c->num_cu = cus;
     c->max_blocks = kNaturalGrid;
@@ -414,6 +438,18 @@ int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks) {
     if (!ctx) return SMOL_EINVAL;
     ctx->max_blocks = max_blocks ? max_blocks : kNaturalGrid;
     ctx->max_blocks_set = max_blocks != 0;
+    return SMOL_OK;
+}
+
+int smol_csum_tool_set_xcd_remap(smol_csum_ctx_t* ctx, int on) {
+    if (!ctx || (on != 0 && on != 1)) return SMOL_EINVAL;
+    ctx->xcd_remap = on;
+    return SMOL_OK;
+}
+
+int smol_csum_tool_set_launch_records(smol_csum_ctx_t* ctx, uint64_t records) {
+    if (!ctx) return SMOL_EINVAL;
+    ctx->launch_records = records;
     return SMOL_OK;
 }
 

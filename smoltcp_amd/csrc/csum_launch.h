@@ -49,7 +49,17 @@ struct KParams {
     const uint8_t* src;             // MODE_COPY: payload source buffer
     const smol_csum_copy_t* copy;   // MODE_COPY: one payload copy per record (16-B aligned)
     const uint8_t* addrs;  // 6LoWPAN NHC UDP batches: 32 B (IPv6 src, dst) per record, else nullptr
+    uint32_t xcd_remap;    // walk kernel: block b takes the records of block xcd_block(b) (see csum_walk.h)
 };
+
+// The 8 XCDs of an MI355X are dealt workgroups round-robin (MI355X_MICROARCH.md, workgroup dispatch:
+// observed, not promised): blocks b, b + 8, ... share an XCD.  This bijection on [0, nwg) gives the
+// blocks of one XCD a contiguous range of logical blocks, so that each XCD streams its own part of
+// the batch (its L2 and address-translation caches see one region instead of every region).
+__host__ __device__ inline uint64_t xcd_block(uint64_t b, uint64_t nwg) {
+    const uint64_t q = nwg / 8, r = nwg % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
 
 // A dispatch may hold at most 2^32 - 1 work-items: 256-thread grids are capped at 2^24 - 1 blocks
 // (every kernel loops with a grid stride, so a capped grid still covers the whole batch; C5's 2^27

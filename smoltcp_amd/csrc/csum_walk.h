@@ -1109,9 +1109,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MinWaves<VA
     }
     // SEGB: a natural grid (one record per group) and a full workgroup, the same for every wave of
     // the workgroup, so that each of them reaches the barrier after the parse exactly once
-    const bool blockwide = SEGB && ngroups >= p.n && (uint64_t)blockIdx.x * GPB + GPB <= p.n;
+    const uint64_t bid = p.xcd_remap ? xcd_block(blockIdx.x, gridDim.x) : (uint64_t)blockIdx.x;
+    const bool blockwide = SEGB && ngroups >= p.n && bid * GPB + GPB <= p.n;
     Walk w;
-    w.r = (uint64_t)blockIdx.x * GPB + gib;
+    w.r = bid * GPB + gib;
     if (w.r >= p.n) return;
     w.cur = rec_at<IMPLICIT, COPY, NHC>(p, w.r);
     w.nxt = rec_at<IMPLICIT, COPY, NHC>(p, w.r + ngroups < p.n ? w.r + ngroups : p.n - 1);

@@ -605,3 +605,113 @@ def test_pretty_print_annotations(eng, golden):
     for f, s in zip(golden["fuzz_corpus_frames"], st[1:]):
         want = " (partial checksum correct)" if f["name"] in partial else ""
         assert checksum.l4_annotation(int(s)) == want, f["name"]
+
+
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_xcd_remap(eng, xcd):
+    """The XCD-contiguous block order (smol_csum_tool_set_xcd_remap) is a bijection on the grid's
+    blocks: emit / verify over fixed-stride and descriptor batches whose block counts are and are not
+    multiples of 8 match the oracle, natural and capped grids."""
+    rng = np.random.default_rng(91)
+    eng.set_xcd_remap(xcd)
+    try:
+        for n in (1, 31, 32 * 8, 32 * 8 + 1, 32 * 13 + 5, 4099):
+            L = 1500
+            buf = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+            batch = E.Batch.fixed(n, L, L, E.KIND_IP)
+            eng.synth(buf, batch, E.SYNTH_UDP4, seed=n)
+            eng.corrupt(buf, batch, every=5, seed=n)
+            host = buf.cpu().numpy().copy()
+            ref_v = oracle.batch_verify(host.copy(), None, n, L, L, E.KIND_IP, CAPS_DEFAULT)
+            ref_e = host.copy()
+            oracle.batch_emit(ref_e, None, n, L, L, E.KIND_IP, CAPS_DEFAULT)
+            for blocks in (0, 3, 9):
+                eng.set_max_blocks(blocks)
+                try:
+                    st = eng.verify(buf, batch).cpu().numpy()
+                    d2 = buf.clone()
+                    eng.emit(d2, batch)
+                finally:
+                    eng.set_max_blocks(0)
+                assert np.array_equal(st, ref_v), (xcd, n, blocks)
+                assert np.array_equal(d2.cpu().numpy(), ref_e), (xcd, n, blocks)
+        recs = [P.ipv4(V4A, V4B, 6, P.tcp(1, 2, P.rand_bytes(rng, int(rng.integers(0, 3000))))) for _ in range(1029)]
+        _run_records(eng, recs, E.KIND_IP, gap_seed=4)
+    finally:
+        eng.set_xcd_remap(0)
+
+
+def test_launch_records(eng):
+    """Batches split into consecutive launches (smol_csum_tool_set_launch_records): emit, verify
+    and data over fixed-stride and descriptor batches, status arrays, copy-emit and 6LoWPAN NHC UDP,
+    chunk sizes that do and do not divide the batch, against the oracle and the unsplit launch."""
+    rng = np.random.default_rng(17)
+    recs = []
+    for i in range(1037):
+        pl = P.rand_bytes(rng, int(rng.integers(0, 1800)))
+        recs.append(P.ipv4(V4A, V4B, 17, P.udp(1000 + i, 53, pl)) if i % 3 else
+                    P.ipv6(bytes(16), bytes([1] * 16), 6, P.tcp(1, 2, pl)))
+    L = 1500
+    n = 2051
+    fixed_buf = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+    fixed = E.Batch.fixed(n, L, L, E.KIND_IP)
+    eng.synth(fixed_buf, fixed, E.SYNTH_UDP4, seed=3)
+    eng.corrupt(fixed_buf, fixed, every=9, seed=3)
+    host = fixed_buf.cpu().numpy().copy()
+    ref_v = oracle.batch_verify(host.copy(), None, n, L, L, E.KIND_IP, CAPS_DEFAULT)
+    ref_e = host.copy()
+    ref_es = oracle.batch_emit(ref_e, None, n, L, L, E.KIND_IP, CAPS_DEFAULT)
+    ref_d = oracle.batch_data(host.copy(), None, n, L, L)
+    for per in (1, 7, 256, 1000, 2051, 5000):
+        eng.set_launch_records(per)
+        try:
+            st = eng.verify(fixed_buf, fixed).cpu().numpy()
+            d2 = fixed_buf.clone()
+            est = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+            eng.emit(d2, fixed, status=est)
+            dat = eng.data(fixed_buf, fixed).cpu().numpy()
+            _run_records(eng, recs, E.KIND_IP, gap_seed=per)
+        finally:
+            eng.set_launch_records(0)
+        assert np.array_equal(st, ref_v), per
+        assert np.array_equal(d2.cpu().numpy(), ref_e), per
+        assert np.array_equal(est.cpu().numpy(), ref_es), per
+        assert np.array_equal(dat, ref_d), per
+
+
+def test_launch_records_copy_and_nhc(eng):
+    """The split launches advance the copy descriptors and the NHC address rows with the records."""
+    rng = np.random.default_rng(29)
+    n, L = 1029, 1500
+    buf = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+    batch = E.Batch.fixed(n, L, kind=E.KIND_IP)
+    eng.synth(buf, batch, E.SYNTH_UDP4, seed=11)
+    host = buf.cpu().numpy().copy()
+    src = rng.integers(0, 256, n * 1472 + 16, dtype=np.uint8)
+    copies = E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472)
+    ref = host.copy()
+    oracle.batch_copy_emit(ref, None, n, src, copies, L, L, E.KIND_IP)
+    recs = [P.nhc_udp(rng, i % 4, bool((i >> 2) & 1), int(rng.integers(0, 300))) for i in range(777)]
+    nbuf, offs, lens = P.pack(recs, gap_rng=rng)
+    addrs = rng.integers(0, 256, (len(recs), 32), dtype=np.uint8)
+    nbatch = E.Batch.from_records(offs, lens, E.KIND_RAW, "cuda:0")
+    desc = P.oracle_desc(offs, lens, 0)
+    ref_nv = oracle.batch_nhc_udp_verify(nbuf.copy(), desc, len(recs), addrs)
+    ref_n = nbuf.copy()
+    oracle.batch_nhc_udp_emit(ref_n, desc, len(recs), addrs)
+    d_addrs = torch.from_numpy(addrs.reshape(-1).copy()).cuda()
+    for per in (5, 64, 1000):
+        eng.set_launch_records(per)
+        try:
+            d = torch.from_numpy(host.copy()).cuda()
+            eng.copy_emit(d, batch, torch.from_numpy(src).cuda(), torch.from_numpy(copies.view(np.uint8).copy()).cuda())
+            got = d.cpu().numpy()
+            dn = torch.from_numpy(nbuf.copy()).cuda()
+            nst = eng.nhc_udp_verify(dn, nbatch, d_addrs).cpu().numpy()
+            eng.nhc_udp_emit(dn, nbatch, d_addrs)
+            gotn = dn.cpu().numpy()
+        finally:
+            eng.set_launch_records(0)
+        assert np.array_equal(got, ref), per
+        assert np.array_equal(nst, ref_nv), per
+        assert np.array_equal(gotn, ref_n), per
