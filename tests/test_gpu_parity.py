@@ -676,7 +676,7 @@ def test_launch_records(eng):
         assert np.array_equal(st, ref_v), per
         assert np.array_equal(d2.cpu().numpy(), ref_e), per
         assert np.array_equal(est.cpu().numpy(), ref_es), per
-        assert np.array_equal(dat, ref_d), per
+        assert np.array_equal(dat.view(np.uint16), ref_d), per
 
 
 def test_launch_records_copy_and_nhc(eng):
