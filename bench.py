@@ -58,7 +58,8 @@ def parse_args(argv=None):
                     help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
     ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
     ap.add_argument("--variant", type=int, default=-1, help="force a kernel variant (tuning)")
-    ap.add_argument("--xcd-remap", type=int, default=-1, help="1/0: force the XCD-contiguous block order (tuning)")
+    ap.add_argument("--xcd-remap", type=int, default=-1, help="1/0: force the XCD-contiguous block order (tuning; "
+                                                               "-1: the library's choice)")
     ap.add_argument("--launch-records", type=int, default=-1, help="records per kernel launch (tuning; 0: all)")
     ap.add_argument("--probe", action="store_true", help="(kept for old scripts: the probes always run)")
     ap.add_argument("--dry-run", action="store_true",
@@ -586,8 +587,7 @@ def main(argv=None):
         eng.set_shape(args.shape)
     if args.variant >= 0:
         eng.set_variant(args.variant)
-    if args.xcd_remap >= 0:
-        eng.set_xcd_remap(args.xcd_remap)
+    eng.set_xcd_remap(args.xcd_remap)
     if args.launch_records >= 0:
         eng.set_launch_records(args.launch_records)
     wl = Workload(E, eng, args.config, args.n, rank, dev)

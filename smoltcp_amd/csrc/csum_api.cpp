@@ -24,7 +24,8 @@ struct smol_csum_ctx {
     uint8_t* dummy;       // 256 zero bytes on the device (target of loads with nothing to read)
     int tile_records;     // tile kernel: records per wavefront tile (32 or 64)
     bool max_blocks_set;  // grid cap given explicitly (tooling)
-    int xcd_remap;        // walk kernel: each XCD's blocks take a contiguous range of records (tooling)
+    int xcd_remap;        // walk kernel: each XCD's blocks take a contiguous range of records
+                          // (-1: automatic, xcd_remap_auto; 0 / 1: forced, tooling)
     uint64_t launch_records;  // records per kernel launch (0: the whole batch in one launch)
 };
 
@@ -99,6 +100,16 @@ int walk_variant(int mode, bool has_desc) {
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
+// The XCD-contiguous block order (csum_launch.h xcd_block) when none is forced: for fixed-stride
+// emit over at least 4 GiB.  Measured per 2^20 C2 records (tools/exp_inplace.py, one box,
+// profiles/r04_experiments/xcd_remap.jsonl): emit 0.327 -> 0.298 ms at 2^22 records (6.3 GB),
+// 0.332 -> 0.320 at 2^24, 0.338 -> 0.303 at 2^26, and C5's 2^27: 0.334 -> 0.300; at 2^20 records
+// 0.297 -> 0.2995 (no gain).  Verify runs 4-6 % slower with it at every size, so it keeps the
+// dispatch order.
+int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
+    return mode == MODE_EMIT && !b->desc && b->n * b->stride >= (4ull << 30) ? 1 : 0;
+}
+
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29) return 5;
@@ -164,7 +175,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.status = d_status;
     p.dummy = ctx->dummy;
     p.num_cu = ctx->max_blocks_set ? 0u : (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256);
-    p.xcd_remap = (uint32_t)ctx->xcd_remap;
+    p.xcd_remap = ctx->xcd_remap >= 0 ? (uint32_t)ctx->xcd_remap : (uint32_t)xcd_remap_auto(mode, b);
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
     // Variants: 0-2, 5-6 = walk kernel (csum_walk.h VarT: load policy, prefetch, chunk
@@ -259,7 +270,7 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     c->dummy = dummy;
     c->tile_records = 32;
     c->max_blocks_set = false;
-    c->xcd_remap = 0;
+    c->xcd_remap = -1;
     c->launch_records = 0;
     c->device = device;
     c->num_cu = cus;
@@ -442,7 +453,7 @@ int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks) {
 }
 
 int smol_csum_tool_set_xcd_remap(smol_csum_ctx_t* ctx, int on) {
-    if (!ctx || (on != 0 && on != 1)) return SMOL_EINVAL;
+    if (!ctx || on < -1 || on > 1) return SMOL_EINVAL;
     ctx->xcd_remap = on;
     return SMOL_OK;
 }

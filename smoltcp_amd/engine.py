@@ -319,8 +319,9 @@ class ChecksumEngine:
         code = {"data": 0, "emit": 1, "verify": 2, "copy_emit": 3}[op]
         return lib().smol_csum_tool_kernel_name(self._h, code, int(bool(has_desc))).decode()
 
-    def set_xcd_remap(self, on: bool):
-        check(lib().smol_csum_tool_set_xcd_remap(self._h, int(bool(on))), "smol_csum_tool_set_xcd_remap")
+    def set_xcd_remap(self, on: int):
+        """1 / 0: force the XCD-contiguous block order on / off; -1: the library's choice."""
+        check(lib().smol_csum_tool_set_xcd_remap(self._h, int(on)), "smol_csum_tool_set_xcd_remap")
 
     def set_launch_records(self, records: int):
         check(lib().smol_csum_tool_set_launch_records(self._h, int(records)), "smol_csum_tool_set_launch_records")

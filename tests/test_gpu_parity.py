@@ -638,7 +638,7 @@ def test_xcd_remap(eng, xcd):
         recs = [P.ipv4(V4A, V4B, 6, P.tcp(1, 2, P.rand_bytes(rng, int(rng.integers(0, 3000))))) for _ in range(1029)]
         _run_records(eng, recs, E.KIND_IP, gap_seed=4)
     finally:
-        eng.set_xcd_remap(0)
+        eng.set_xcd_remap(-1)
 
 
 def test_launch_records(eng):

@@ -10,7 +10,8 @@ Sequences, each timed per kernel with HIP events on one stream, interleaved roun
   verify  verify A, verify A    (verify only)
   vv      verify A, verify B    (two read-only passes over different buffers)
   ev_swap emit A, verify B, emit B, verify A  (emit's buffer verified one kernel later)
-Usage: exp_inplace.py [n_records] [seq,seq,...]   (SIZES="17,18,..." runs log2 sizes in turn)"""
+Usage: exp_inplace.py [n_records] [seq,seq,...]   (SIZES="17,18,..." runs log2 sizes in turn;
+XCD_EMIT / XCD_VERIFY = 1: that kernel with the XCD-contiguous block order)"""
 import json
 import os
 import sys
@@ -47,10 +48,14 @@ def run(n, only):
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
 
+    xe, xv = int(os.environ.get("XCD_EMIT", "-1")), int(os.environ.get("XCD_VERIFY", "-1"))
+
     def emit(x):
+        eng.set_xcd_remap(xe)
         eng.emit(bufs[x], b)
 
     def verify(x):
+        eng.set_xcd_remap(xv)
         eng.verify(bufs[x], b, status=st)
 
     seqs = {
@@ -88,7 +93,7 @@ def run(n, only):
             for kind, a, z in evs:
                 per.setdefault(kind, []).append(a.elapsed_time(z))
             if rnd:
-                print(json.dumps({"round": rnd, "seq": name, "n": n,
+                print(json.dumps({"round": rnd, "seq": name, "n": n, "xcd_emit": xe, "xcd_verify": xv,
                                   **{f"{k}_ms": round(sum(v) / len(v), 4) for k, v in per.items()}}), flush=True)
 
 
