@@ -453,7 +453,7 @@ int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks) {
 }
 
 int smol_csum_tool_set_xcd_remap(smol_csum_ctx_t* ctx, int on) {
-    if (!ctx || on < -1 || on > 1) return SMOL_EINVAL;
+    if (!ctx || on < -1) return SMOL_EINVAL;
     ctx->xcd_remap = on;
     return SMOL_OK;
 }

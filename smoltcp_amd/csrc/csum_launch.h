@@ -49,7 +49,8 @@ struct KParams {
     const uint8_t* src;             // MODE_COPY: payload source buffer
     const smol_csum_copy_t* copy;   // MODE_COPY: one payload copy per record (16-B aligned)
     const uint8_t* addrs;  // 6LoWPAN NHC UDP batches: 32 B (IPv6 src, dst) per record, else nullptr
-    uint32_t xcd_remap;    // walk kernel: block b takes the records of block xcd_block(b) (see csum_walk.h)
+    uint32_t xcd_remap;    // walk kernel: 0 dispatch order; 1 block b takes the records of block
+                           // xcd_block(b); K >= 2: those of xcd_chunk(b, K) (see below)
 };
 
 // The 8 XCDs of an MI355X are dealt workgroups round-robin (MI355X_MICROARCH.md, workgroup dispatch:
@@ -59,6 +60,16 @@ struct KParams {
 __host__ __device__ inline uint64_t xcd_block(uint64_t b, uint64_t nwg) {
     const uint64_t q = nwg / 8, r = nwg % 8, x = b % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// The same at a finer grain: the XCDs take turns over runs of K consecutive logical blocks (K = 1 is
+// the dispatch order).  A bijection: the first nwg rounded down to 8K blocks are permuted, the rest
+// keep their index.
+__host__ __device__ inline uint64_t xcd_chunk(uint64_t b, uint64_t nwg, uint64_t K) {
+    const uint64_t full = nwg / (8 * K) * (8 * K);
+    if (b >= full) return b;
+    const uint64_t x = b % 8, j = b / 8;
+    return ((j / K) * 8 + x) * K + (j % K);
 }
 
 // A dispatch may hold at most 2^32 - 1 work-items: 256-thread grids are capped at 2^24 - 1 blocks

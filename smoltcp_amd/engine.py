@@ -320,7 +320,8 @@ class ChecksumEngine:
         return lib().smol_csum_tool_kernel_name(self._h, code, int(bool(has_desc))).decode()
 
     def set_xcd_remap(self, on: int):
-        """1 / 0: force the XCD-contiguous block order on / off; -1: the library's choice."""
+        """1 / 0: force the XCD-contiguous block order on / off; K >= 2: runs of K workgroups per XCD
+        turn; -1: the library's choice."""
         check(lib().smol_csum_tool_set_xcd_remap(self._h, int(on)), "smol_csum_tool_set_xcd_remap")
 
     def set_launch_records(self, records: int):

@@ -607,7 +607,7 @@ def test_pretty_print_annotations(eng, golden):
         assert checksum.l4_annotation(int(s)) == want, f["name"]
 
 
-@pytest.mark.parametrize("xcd", [0, 1])
+@pytest.mark.parametrize("xcd", [0, 1, 2, 7, 64])
 def test_xcd_remap(eng, xcd):
     """The XCD-contiguous block order (smol_csum_tool_set_xcd_remap) is a bijection on the grid's
     blocks: emit / verify over fixed-stride and descriptor batches whose block counts are and are not
