@@ -58,6 +58,13 @@ def test_cpp_scalar_mirrors(binary, tmp_path, golden):
     assert f"vectors {len(lines)}" in r.stdout
 
 
+def test_grid_orders_bijective(binary):
+    """The walk kernel's XCD block orders (csum_launch.h xcd_block / xcd_chunk) visit every block
+    once for every grid size (host build of the same header)."""
+    r = subprocess.run([os.path.join(CPP, "test_grid_order")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "grid orders ok" in r.stdout, r.stdout + r.stderr
+
+
 def test_cpp_engine_fails_loudly_without_device(binary):
     if _has_gpu():
         pytest.skip("a GPU is present")
