@@ -692,9 +692,6 @@ def main(argv=None):
         wl.tx[addrs] = saved[0]
         wl.tx[addrs + 1] = saved[1]
         del saved
-        # the same stream with the 64-B segment around each field rewritten whole (values unchanged):
-        # the store shape of whole-segment emit, every segment, no race check
-        seg_ms = timed(lambda: eng.field_probe_list(wl.tx, addrs, first, seg64=True, stream=stream))
         del addrs, first
         torch.cuda.synchronize()
         nbytes = wl.tx.numel() // 16 * 16
@@ -704,10 +701,7 @@ def main(argv=None):
                  "what": "the 2-B-store reference: the TX buffer streamed once (best read pattern) + " + where
                          + " (emit's store events as 2-B writes, no parse / gates); fixed-stride emit writes "
                          "whole 64-B field segments (variant 29) and runs under it; the bytes the probe "
-                         "overwrote are restored",
-                 "seg64_ms": round(seg_ms, 4),
-                 "seg64_what": "the same stream with the 64-B segment holding each checksum field rewritten "
-                               "whole (its own values): the floor of a whole-segment emit"}
+                         "overwrote are restored"}
 
     # Fresh batches (rank 0, batches of at most 4 GB): the timed steps re-emit the same TX batch, and
     # the ~70 MB of field segments one C2 pass writes stay dirty in the 256-MB Infinity Cache, where
