@@ -61,19 +61,20 @@ namespace smolcsum {
 template <int VAR>
 struct VarT {
     static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                               (VAR >= 23 && VAR <= 29);
+                               (VAR >= 23 && VAR <= 30);
     static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 26 && VAR != 27 &&
                                VAR != 28;
     static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                                 (VAR >= 23 && VAR <= 29);
+                                 (VAR >= 23 && VAR <= 30);
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
     static constexpr bool SHUF2 = VAR == 16;
-    static constexpr bool SEGW = VAR == 19 || VAR == 29;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
-    // 29 = 19 with the segment machinery skipped on wavefronts that hold no IPv4 record (a ballot after
-    // the parse: IPv6 records have one field and keep the 2-B store)
-    static constexpr bool SEGW_BALLOT = VAR == 29;
+    static constexpr bool SEGW = VAR == 19 || VAR == 29 || VAR == 30;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
+    // SEGOPT bit 0 (29): the segment machinery skipped on wavefronts that hold no IPv4 record (a
+    // ballot after the parse: IPv6 records have one field and keep the 2-B store); bit 1 (30 = 29 +):
+    // the segments stored with non-temporal stores
+    static constexpr int SEGOPT = VAR == 29 ? 1 : VAR == 30 ? 3 : 0;
     // 23-27 (emit): whole 64-B field segments with the neighbours' record extents published too, so
     // that they serve descriptor batches as well as fixed strides (SEGG); SEGB: the neighbours of the
     // whole workgroup, not only of the wavefront (a workgroup barrier after the parse, natural grid);
@@ -607,7 +608,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
           bool SHUF = false, bool WHOLE = false, bool SHUF2 = false, bool SEGW = false, bool SEGG = false,
-          bool SEGB = false, bool SEG6 = false, bool SEGW_BALLOT = false>
+          bool SEGB = false, bool SEG6 = false, int SEGOPT = 0>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib, SegInfo* si = nullptr, SegInfoG* sg = nullptr,
@@ -761,7 +762,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             // the lanes sum [0, span_end): the header part is subtracted at the end
             w.s1 = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? (int)g.span_end : 0;
             if constexpr (SEGW) w.segA = w.segB = SEG_NONE;
-            if (SEGW && (!SEGW_BALLOT || __any(g.fam == 4))) {
+            if (SEGW && (!(SEGOPT & 1) || __any(g.fam == 4))) {
                 // publish every field finish_gates may write (a superset is safe), then decide which
                 // of this record's field segments go out whole (see the finish below)
                 uint32_t f[3], lo = NO_FIELD, hi = 0;
@@ -1014,14 +1015,13 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                 if (wsA != ~0ull || wsB != ~0ull) {
                     wave_lds_sync();
                     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-                    if (wsA != ~0ull && lane < 8) {
-                        const uint64_t d = wsA + 8u * (uint32_t)lane;
-                        *(GMEM u32x2*)d = *reinterpret_cast<const u32x2*>(winb + (d - base));
-                    }
-                    if (wsB != ~0ull && lane < 8) {
-                        const uint64_t d = wsB + 8u * (uint32_t)lane;
-                        *(GMEM u32x2*)d = *reinterpret_cast<const u32x2*>(winb + (d - base));
-                    }
+                    auto seg_store = [&](uint64_t d) {
+                        const u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - base));
+                        if constexpr (SEGOPT & 2) __builtin_nontemporal_store(x, (GMEM u32x2*)d);
+                        else *(GMEM u32x2*)d = x;
+                    };
+                    if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
+                    if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
                     wave_lds_sync();  // the window is rewritten by the group's next record
                 }
             }
@@ -1139,9 +1139,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MinWaves<VA
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
             if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6,
-                           VarT<VAR>::SEGW_BALLOT>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
+                           VarT<VAR>::SEGOPT>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
             if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6,
-                           VarT<VAR>::SEGW_BALLOT>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
+                           VarT<VAR>::SEGOPT>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
         }
     } else {
         while (true) {
@@ -1208,7 +1208,10 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
         case 19: return launch_shape<MODE, IMPLICIT, 19>(shape, p, max_blocks, s);
         case 29:
-            if constexpr (MODE == MODE_EMIT && IMPLICIT) return launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s);
+        case 30:
+            if constexpr (MODE == MODE_EMIT && IMPLICIT)
+                return var == 29 ? launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s)
+                                 : launch_seg_shape<IMPLICIT, 30>(shape, p, max_blocks, s);
             return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 23:
         case 24:
@@ -1246,7 +1249,7 @@ template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
     // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
-    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 29)) {
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 30)) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
