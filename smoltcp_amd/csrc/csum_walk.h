@@ -61,20 +61,20 @@ namespace smolcsum {
 template <int VAR>
 struct VarT {
     static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                               (VAR >= 23 && VAR <= 30);
+                               (VAR >= 23 && VAR <= 29);
     static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 26 && VAR != 27 &&
                                VAR != 28;
     static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                                 (VAR >= 23 && VAR <= 30);
+                                 (VAR >= 23 && VAR <= 29);
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
     static constexpr bool SHUF2 = VAR == 16;
-    static constexpr bool SEGW = VAR == 19 || VAR == 29 || VAR == 30;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
+    static constexpr bool SEGW = VAR == 19 || VAR == 29;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
     // SEGOPT bit 0 (29): the segment machinery skipped on wavefronts that hold no IPv4 record (a
-    // ballot after the parse: IPv6 records have one field and keep the 2-B store); bit 1 (30 = 29 +):
-    // the segments stored with non-temporal stores
-    static constexpr int SEGOPT = VAR == 29 ? 1 : VAR == 30 ? 3 : 0;
+    // ballot after the parse: IPv6 records have one field and keep the 2-B store).  (Round 4 also
+    // measured the segments stored non-temporal: C2 emit 0.303 against 0.296 ms; removed.)
+    static constexpr int SEGOPT = VAR == 29 ? 1 : 0;
     // 23-27 (emit): whole 64-B field segments with the neighbours' record extents published too, so
     // that they serve descriptor batches as well as fixed strides (SEGG); SEGB: the neighbours of the
     // whole workgroup, not only of the wavefront (a workgroup barrier after the parse, natural grid);
@@ -1016,9 +1016,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                     wave_lds_sync();
                     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
                     auto seg_store = [&](uint64_t d) {
-                        const u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - base));
-                        if constexpr (SEGOPT & 2) __builtin_nontemporal_store(x, (GMEM u32x2*)d);
-                        else *(GMEM u32x2*)d = x;
+                        *(GMEM u32x2*)d = *reinterpret_cast<const u32x2*>(winb + (d - base));
                     };
                     if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
                     if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
@@ -1208,10 +1206,7 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
         case 19: return launch_shape<MODE, IMPLICIT, 19>(shape, p, max_blocks, s);
         case 29:
-        case 30:
-            if constexpr (MODE == MODE_EMIT && IMPLICIT)
-                return var == 29 ? launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s)
-                                 : launch_seg_shape<IMPLICIT, 30>(shape, p, max_blocks, s);
+            if constexpr (MODE == MODE_EMIT && IMPLICIT) return launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s);
             return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 23:
         case 24:
@@ -1249,7 +1244,7 @@ template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
     // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
-    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 30)) {
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 29)) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
