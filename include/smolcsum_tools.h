@@ -65,7 +65,7 @@ int smol_csum_tool_set_tile(smol_csum_ctx_t* ctx, int records);
 /* Cap the number of workgroups per launch (0 = automatic: CUs x 8). */
 int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
 
-/* Walk-kernel launches with on = 1 map workgroup b to the records of workgroup xcd_block(b)
+/* Walk-, tile- and copy-kernel launches with on = 1 map workgroup b to the records of workgroup xcd_block(b)
  * (csum_launch.h): the workgroups that share an XCD take one contiguous range of the batch.  on = K
  * >= 2: the XCDs take turns over runs of K workgroups (xcd_chunk).  0: the natural order.  -1 (the
  * default): the library's choice (on for fixed-stride emit over >= 4 GiB). */

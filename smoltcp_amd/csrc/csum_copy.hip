@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     const uint8_t* winb = reinterpret_cast<const uint8_t*>(wn);
     const uint64_t dummy = (uint64_t)p.dummy;
 
-    for (uint64_t r = (uint64_t)blockIdx.x * GPB + gib; r < p.n; r += ngroups) {
+    for (uint64_t r = logical_block(p.xcd_remap) * GPB + gib; r < p.n; r += ngroups) {
         const RecRef rr = rec_at<IMPLICIT, true>(p, r);
         if (rr.kind & KIND_BAD_COPY) {  // the copy range does not fit: record left untouched
             if (lane == 0 && p.status) ((gu8)p.status)[r] = (uint8_t)SMOL_ST_MALFORMED;

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
     const uint64_t dummy = (uint64_t)p.dummy;
 
-    for (uint64_t tile = (uint64_t)blockIdx.x * 4 + wave; tile * TILE < p.n; tile += nwaves) {
+    for (uint64_t tile = logical_block(p.xcd_remap) * 4 + wave; tile * TILE < p.n; tile += nwaves) {
         const uint64_t r0 = tile * TILE;
         const uint32_t cnt = (uint32_t)((p.n - r0) < (uint64_t)TILE ? (p.n - r0) : (uint64_t)TILE);
 

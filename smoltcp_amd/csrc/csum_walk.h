@@ -1107,9 +1107,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MinWaves<VA
     }
     // SEGB: a natural grid (one record per group) and a full workgroup, the same for every wave of
     // the workgroup, so that each of them reaches the barrier after the parse exactly once
-    const uint64_t bid = p.xcd_remap == 0 ? (uint64_t)blockIdx.x
-                         : p.xcd_remap == 1 ? xcd_block(blockIdx.x, gridDim.x)
-                                            : xcd_chunk(blockIdx.x, gridDim.x, p.xcd_remap);
+    const uint64_t bid = logical_block(p.xcd_remap);
     const bool blockwide = SEGB && ngroups >= p.n && bid * GPB + GPB <= p.n;
     Walk w;
     w.r = bid * GPB + gib;

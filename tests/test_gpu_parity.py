@@ -636,7 +636,19 @@ def test_xcd_remap(eng, xcd):
                 assert np.array_equal(st, ref_v), (xcd, n, blocks)
                 assert np.array_equal(d2.cpu().numpy(), ref_e), (xcd, n, blocks)
         recs = [P.ipv4(V4A, V4B, 6, P.tcp(1, 2, P.rand_bytes(rng, int(rng.integers(0, 3000))))) for _ in range(1029)]
-        _run_records(eng, recs, E.KIND_IP, gap_seed=4)
+        _run_records(eng, recs, E.KIND_IP, gap_seed=4)  # verify: walk kernel, emit: tile kernel
+        # copy-emit (copy_kernel) under the same order
+        n, L = 2053, 1500
+        buf = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        batch = E.Batch.fixed(n, L, kind=E.KIND_IP)
+        eng.synth(buf, batch, E.SYNTH_UDP4, seed=xcd)
+        host = buf.cpu().numpy().copy()
+        src = rng.integers(0, 256, n * 1472 + 16, dtype=np.uint8)
+        copies = E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472)
+        eng.copy_emit(buf, batch, torch.from_numpy(src).cuda(), torch.from_numpy(copies.view(np.uint8).copy()).cuda())
+        ref = host.copy()
+        oracle.batch_copy_emit(ref, None, n, src, copies, L, L, E.KIND_IP)
+        assert np.array_equal(buf.cpu().numpy(), ref), xcd
     finally:
         eng.set_xcd_remap(-1)
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Time the fused copy + emit (C2copy workload) per launch shape and kernel variant: one JSON line each.
 
-Usage: exp_copy.py [shapes, e.g. 0,1,3,5] [variants, e.g. 8,11,12]"""
+Usage: [XCD=K] exp_copy.py [shapes, e.g. 0,1,3,5] [variants, e.g. 8,11,12]   (XCD: the block order, see
+smol_csum_tool_set_xcd_remap)"""
 import json
 import os
 import sys
@@ -16,6 +17,7 @@ from smoltcp_amd import engine as E  # noqa: E402
 def main():
     n, L = 1 << 20, 1500
     eng = E.ChecksumEngine(0)
+    eng.set_xcd_remap(int(os.environ.get("XCD", "-1")))
     dev = torch.device("cuda:0")
     tx = torch.empty(n * L, dtype=torch.uint8, device=dev)
     b = E.Batch.fixed(n, L, L, E.KIND_IP)

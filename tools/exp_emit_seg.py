@@ -21,6 +21,7 @@ def main():
     cfgs = (sys.argv[1] if len(sys.argv) > 1 else "c2,c4").split(",")
     dev = torch.device("cuda", 0)
     eng = E.ChecksumEngine(0)
+    eng.set_xcd_remap(int(os.environ.get("XCD", "-1")))
     wls = {c: bench.Workload(E, eng, c, 0, 0, dev) for c in cfgs}
     torch.cuda.synchronize()
     def vars_of(c):
