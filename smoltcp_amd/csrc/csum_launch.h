@@ -72,12 +72,14 @@ __host__ __device__ inline uint64_t xcd_chunk(uint64_t b, uint64_t nwg, uint64_t
     return ((j / K) * 8 + x) * K + (j % K);
 }
 
+#ifdef __HIPCC__
 // The logical block this workgroup works as (KParams::xcd_remap).
 __device__ inline uint64_t logical_block(uint32_t xcd_remap) {
     return xcd_remap == 0 ? (uint64_t)blockIdx.x
            : xcd_remap == 1 ? xcd_block(blockIdx.x, gridDim.x)
                             : xcd_chunk(blockIdx.x, gridDim.x, xcd_remap);
 }
+#endif
 
 // A dispatch may hold at most 2^32 - 1 work-items: 256-thread grids are capped at 2^24 - 1 blocks
 // (every kernel loops with a grid stride, so a capped grid still covers the whole batch; C5's 2^27
