@@ -112,14 +112,14 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
-    if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 32) return 5;
+    if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29) return 5;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
 
 bool line_grid(int variant) {
     return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 19 ||
-           (variant >= 23 && variant <= 29) || variant == 31 || variant == 32;
+           (variant >= 23 && variant <= 29);
 }
 
 int auto_shape(uint32_t len, bool has_desc, bool line = false, int variant = -1) {
@@ -434,7 +434,7 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
 }
 
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 32) return SMOL_EINVAL;
+    if (!ctx || variant < -1 || variant > 29) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

@@ -61,20 +61,20 @@ namespace smolcsum {
 template <int VAR>
 struct VarT {
     static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                               (VAR >= 23 && VAR <= 29) || VAR == 31 || VAR == 32;
+                               (VAR >= 23 && VAR <= 29);
     static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 26 && VAR != 27 &&
                                VAR != 28;
     static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                                 (VAR >= 23 && VAR <= 29) || VAR == 31 || VAR == 32;
+                                 (VAR >= 23 && VAR <= 29);
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
     static constexpr bool SHUF2 = VAR == 16;
-    static constexpr bool SEGW = VAR == 19 || VAR == 29 || VAR == 32;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
+    static constexpr bool SEGW = VAR == 19 || VAR == 29;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
     // SEGOPT bit 0 (29): the segment machinery skipped on wavefronts that hold no IPv4 record (a
     // ballot after the parse: IPv6 records have one field and keep the 2-B store).  (Round 4 also
     // measured the segments stored non-temporal: C2 emit 0.303 against 0.296 ms; removed.)
-    static constexpr int SEGOPT = (VAR == 29 || VAR == 32) ? 1 : 0;
+    static constexpr int SEGOPT = VAR == 29 ? 1 : 0;
     // 23-27 (emit): whole 64-B field segments with the neighbours' record extents published too, so
     // that they serve descriptor batches as well as fixed strides (SEGG); SEGB: the neighbours of the
     // whole workgroup, not only of the wavefront (a workgroup barrier after the parse, natural grid);
@@ -1067,8 +1067,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 // 16 x 4 (descriptor batches); the segment decision's registers otherwise cost it two waves.
 template <int VAR, int MODE>
 struct MinWaves {
-    static constexpr int value = (MODE == MODE_EMIT && VAR == 28) ? 7
-                                 : ((MODE == MODE_VERIFY && VAR == 31) || (MODE == MODE_EMIT && VAR == 32)) ? 5 : 1;
+    static constexpr int value = (MODE == MODE_EMIT && VAR == 28) ? 7 : 1;
 };
 
 template <int G, int U, int MODE, bool IMPLICIT, int VAR, bool NHC = false>
@@ -1207,35 +1206,6 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 29:
             if constexpr (MODE == MODE_EMIT && IMPLICIT) return launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s);
             return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
-        case 32:  // variant 29 held to 5 waves per SIMD (emit, experiment)
-            if constexpr (MODE == MODE_EMIT && IMPLICIT) {
-                if (shape == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 32>(p, max_blocks, s);
-                return launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s);
-            }
-            return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
-        case 31:  // variant 5 held to 5 waves per SIMD (verify, experiment)
-            if constexpr (MODE == MODE_VERIFY && IMPLICIT) {
-                if (shape == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 31>(p, max_blocks, s);
-            }
-            return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
-        case 23:
-        case 24:
-        case 25:
-        case 26:
-        case 27:
-        case 28:
-            if constexpr (MODE == MODE_EMIT) {
-                switch (var) {
-                    case 23: return launch_seg_shape<IMPLICIT, 23>(shape, p, max_blocks, s);
-                    case 24: return launch_seg_shape<IMPLICIT, 24>(shape, p, max_blocks, s);
-                    case 25: return launch_seg_shape<IMPLICIT, 25>(shape, p, max_blocks, s);
-                    case 26: return launch_seg_shape<IMPLICIT, 26>(shape, p, max_blocks, s);
-                    case 27: return launch_seg_shape<IMPLICIT, 27>(shape, p, max_blocks, s);
-                    default: return launch_seg_shape<IMPLICIT, 28>(shape, p, max_blocks, s);
-                }
-            }
-            return var >= 26 ? launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s)
-                             : launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 9:
         case 10:
             if constexpr (MODE == MODE_EMIT && IMPLICIT) {
@@ -1254,7 +1224,7 @@ template <int MODE, bool IMPLICIT>
 hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const int g = (shape == CFG_G8U6 || shape == CFG_G8U7) ? shape : CFG_G16U3;
     // the line-grid variants (the descriptor-verify default 13 included) run variant 5 here
-    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 29) || var == 31 || var == 32) {
+    if (var == 5 || var == 6 || var == 9 || var == 10 || var == 13 || var == 19 || (var >= 23 && var <= 29)) {
         if (g == CFG_G8U6) return launch_one<8, 6, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         if (g == CFG_G8U7) return launch_one<8, 7, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
         return launch_one<16, 3, MODE, IMPLICIT, 5, true>(p, max_blocks, s);
