@@ -68,7 +68,8 @@ int smol_csum_tool_set_max_blocks(smol_csum_ctx_t* ctx, uint32_t max_blocks);
 /* Walk-, tile- and copy-kernel launches with on = 1 map workgroup b to the records of workgroup xcd_block(b)
  * (csum_launch.h): the workgroups that share an XCD take one contiguous range of the batch.  on = K
  * >= 2: the XCDs take turns over runs of K workgroups (xcd_chunk).  0: the natural order.  -1 (the
- * default): the library's choice (on for fixed-stride emit over >= 4 GiB). */
+ * default): the library's choice (contiguous for fixed-stride emit over >= 4 GiB, runs of 256 for
+ * fixed-stride verify over >= 64 GiB, the dispatch order otherwise). */
 int smol_csum_tool_set_xcd_remap(smol_csum_ctx_t* ctx, int on);
 
 /* Batched calls over more than `records` records (0: no limit, the default) go out as consecutive

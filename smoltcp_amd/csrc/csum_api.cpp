@@ -100,14 +100,21 @@ int walk_variant(int mode, bool has_desc) {
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
-// The XCD-contiguous block order (csum_launch.h xcd_block) when none is forced: for fixed-stride
-// emit over at least 4 GiB.  Measured per 2^20 C2 records (tools/exp_inplace.py, one box,
+// The XCD block order (csum_launch.h xcd_block / xcd_chunk) when none is forced: the contiguous order
+// for fixed-stride emit over at least 4 GiB.  Measured per 2^20 C2 records (tools/exp_inplace.py, one box,
 // profiles/r04_experiments/xcd_remap.jsonl): emit 0.327 -> 0.298 ms at 2^22 records (6.3 GB),
 // 0.332 -> 0.320 at 2^24, 0.338 -> 0.303 at 2^26, and C5's 2^27: 0.334 -> 0.300; at 2^20 records
 // 0.297 -> 0.2995 (no gain).  Verify runs 4-6 % slower with it at every size, so it keeps the
 // dispatch order.
+// Verify over at least 64 GiB takes runs of 256 workgroups per XCD turn: C5's in-place verify 31.38-
+// 31.46 -> 30.96-30.99 ms (profiles/r04_experiments/c5_verify_grain.jsonl); at 25 GB it was +1 %,
+// at 100 GB -0.6 % (xcd_grain.jsonl), so smaller batches keep the dispatch order.
 int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
-    return mode == MODE_EMIT && !b->desc && b->n * b->stride >= (4ull << 30) ? 1 : 0;
+    if (b->desc) return 0;
+    const uint64_t bytes = b->n * b->stride;
+    if (mode == MODE_EMIT) return bytes >= (4ull << 30) ? 1 : 0;
+    if (mode == MODE_VERIFY) return bytes >= (64ull << 30) ? 256 : 0;
+    return 0;
 }
 
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
