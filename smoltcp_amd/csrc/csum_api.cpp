@@ -223,8 +223,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         // chunks): C2copy 0.772-0.853 ms (variant 16) -> 0.689 ms (tools/exp_copy.py, MI355X).
         // Variants 1 / 8 / 11 / 16 stay selectable.
         const int cv = ctx->variant;
-        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? cv : 17;
-        const int cshape = ctx->shape >= 0 ? ctx->shape : (var == 17 ? (int)CFG_G16U4 : shape);
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 21) ? cv : 17;
+        const int cshape = ctx->shape >= 0 ? ctx->shape : ((var == 17 || var == 21) ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;

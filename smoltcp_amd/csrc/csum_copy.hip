@@ -68,7 +68,10 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 
 }  // namespace copy2
 
-template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0>
+// LBS (variant 21): the first body round's loads are issued right after the parse, before round 1's
+// chunk stores, so that waiting for them does not also wait for those stores (gfx950 counts stores
+// in vmcnt, in issue order with the loads).
+template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0, bool LBS = false>
 __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
     constexpr int GPB = 256 / G;
@@ -235,6 +238,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         }
         const bool far = f0b != NOF || f1b != NOF || f2b != NOF;
         const int len = (int)rr.len;
+        if constexpr (LBS) body_load(UB > 0 ? nbe : body1, blo, bhi);
 
         // ---- sum round 1; store its chunks past the window ----
         uint32_t acc = 0;
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             }
         }
         for (uint32_t i0 = UB > 0 ? nbe : body1; i0 < nb; i0 += (uint32_t)(G * U)) {
-            body_load(i0, blo, bhi);
+            if (!LBS || i0 != (UB > 0 ? nbe : body1)) body_load(i0, blo, bhi);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t i = i0 + (uint32_t)(u * G + lane);
@@ -307,12 +311,12 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     }
 }
 
-template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0>
+template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0, bool LBS = false>
 hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB>), dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB, LBS>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -342,6 +346,16 @@ hipError_t launch_copy2(int shape, const KParams& p, uint32_t max_blocks, hipStr
 
 hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     return p.desc == nullptr ? launch_copy2<true>(shape, p, max_blocks, s) : launch_copy2<false>(shape, p, max_blocks, s);
+}
+
+// variant 21: variant 17's default shapes with the first body round's loads ahead of round 1's stores
+hipError_t launch_copy_v21(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    const bool im = p.desc == nullptr;
+    if (shape == CFG_G16U6)
+        return im ? launch_copy2_one<true, 16, 5, 1, 1, true>(p, max_blocks, s)
+                  : launch_copy2_one<false, 16, 5, 1, 1, true>(p, max_blocks, s);
+    return im ? launch_copy2_one<true, 16, 4, 1, 2, true>(p, max_blocks, s)
+              : launch_copy2_one<false, 16, 4, 1, 2, true>(p, max_blocks, s);
 }
 
 }  // namespace smolcsum

@@ -1256,11 +1256,14 @@ hipError_t launch_copy_var(int shape, const KParams& p, uint32_t max_blocks, hip
 
 // variant 17: the class-split copy-emit kernel (csum_copy.hip)
 hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s);
+// variant 21: variant 17 with the first body round's loads ahead of round 1's stores (csum_copy.hip)
+hipError_t launch_copy_v21(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s);
 
 template <bool IMPLICIT>
 hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (var) {
         case 17: return launch_copy_v17(shape, p, max_blocks, s);
+        case 21: return launch_copy_v21(shape, p, max_blocks, s);
         case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
         case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);
         case 8: return launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);

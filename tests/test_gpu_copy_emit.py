@@ -178,12 +178,12 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
         # the default (17), a capped grid, the prefetch variant (1), the two-load variant (8), the
         # lane-shuffle variants (11, 16)
         for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (8, 0), (8, 7), (16, 0), (16, 7), (17, 0),
-                               (17, 7)):
+                               (17, 7), (21, 0), (21, 7)):
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,
                  base=base, seed=n + variant)
 
 
-COPY_VARIANTS = [-1, 1, 8, 11, 16, 17]
+COPY_VARIANTS = [-1, 1, 8, 11, 16, 17, 21]
 
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
@@ -199,7 +199,7 @@ def test_copy_emit_mixed_packed(eng, shape, variant):
     assert (st & E.ST_MALFORMED).sum() == 0
 
 
-@pytest.mark.parametrize("variant", [-1, 16, 17])
+@pytest.mark.parametrize("variant", [-1, 16, 17, 21])
 def test_copy_emit_packed_zero_gaps(eng, variant):
     """C3-style batch: TCP records of U[64, 9000] bytes packed back to back with no gap (odd
     offsets), so neighbouring records share cache lines.  Copy-emit rewrites every byte of a record
@@ -341,7 +341,7 @@ def test_copy_emit_tiny_records(eng, variant):
         _run(eng, recs, spec, gap_seed=17, seed=18 + shape, variant=variant, shape=shape)
 
 
-@pytest.mark.parametrize("variant", [-1, 16, 17])
+@pytest.mark.parametrize("variant", [-1, 16, 17, 21])
 def test_copy_emit_packed_fields_in_last_line(eng, variant):
     """Records packed back to back (no gaps) where some hold their L4 checksum field in their last
     128-B line (an IPv6 Hop-by-Hop header of 256-2000 B before a short TCP / UDP segment), between
