@@ -39,7 +39,7 @@ int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
 /* Kernel variant (-1 = automatic: 7 for emit over descriptor batches, 13 for verify over
- * descriptor batches, 19 for fixed-stride emit, 5 otherwise; 17 for copy-emit).  The
+ * descriptor batches, 29 for fixed-stride emit, 5 otherwise; 21 for copy-emit).  The
  * "walk" kernel (a group parses and finishes its own record) reads 16-byte chunks on a grid that
  * starts at the record's 16-byte boundary: 0 = non-temporal loads + register prefetch of the next
  * step, 1 = plain (cached) loads + prefetch, 2 = non-temporal loads without prefetch; or at its
@@ -51,12 +51,16 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
  * 16-byte chunk of every lane's step loaded cached, so that the lines holding the fields are
  * resident in L2 when emit stores them (fixed-stride emit only; elsewhere 5).  13 = variant 5
  * without the prefetch.  19 = variant 5 whose emit writes the 64-byte segments holding an IPv4
- * record's fields whole where no neighbouring record's field shares them (the default for
- * fixed-stride emit; elsewhere 5).  Copy-emit: 1 / 8 / 11 / 16 = the walk kernel in its copy mode (prefetch /
- * two aligned source chunks / one chunk + the next lane's / dword-aligned source + one dword from
- * the next lane); 17 (default) = copy_kernel (csum_copy.hip), whose shapes are 16 x 4 with 32 body
- * chunks in round 1 (default, shape 8), 16 x 3 (1), 8 x 6 (0), 8 x 4 (7), 16 x 5 (2), 16 x 4 with
- * the body chunks of round 1 built the generic way (3), 32 x 2 (4), 64 x 2 (5, 6). */
+ * record's fields whole where no neighbouring record's field shares them (fixed-stride emit;
+ * elsewhere 5); 29 = 19 behind a wavefront ballot that skips the segment logic for steps without
+ * an IPv4 record (the default for fixed-stride emit).  23-28 = whole-segment emit generalised to
+ * any record extents (descriptor batches; csum_walk.h).  Copy-emit: 1 / 8 / 11 / 16 = the walk
+ * kernel in its copy mode (prefetch / two aligned source chunks / one chunk + the next lane's /
+ * dword-aligned source + one dword from the next lane); 17 = copy_kernel (csum_copy.hip), whose
+ * shapes are 16 x 4 with 32 body chunks in round 1 (default, shape 8), 16 x 3 (1), 8 x 6 (0),
+ * 8 x 4 (7), 16 x 5 (2), 16 x 4 with the body chunks of round 1 built the generic way (3),
+ * 32 x 2 (4), 64 x 2 (5, 6); 21 (default) = 17 with the first body round's loads issued ahead of
+ * round 1's stores (16 x 4 with 32 body chunks in round 1; shape 2: 16 x 5 with 16). */
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant);
 
 /* Tile kernel: records per wavefront tile, 32 (default) or 64. */
@@ -103,6 +107,11 @@ int smol_csum_tool_auto_shape(uint32_t len, int has_desc);
 /* The kernel (the rocprofv3 name prefix: "csum_kernel" or "csum_tile_kernel") that an IP-path
  * operation runs with this context's variant setting: op 0 data, 1 emit, 2 verify, 3 copy-emit. */
 const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int has_desc);
+
+/* The kernel instantiation of this process's last checksum launch (any context), packed as
+ * kernel << 24 | variant << 16 | G << 8 | U; kernel 1 = csum_kernel, 2 = csum_tile_kernel,
+ * 3 = copy_kernel, 4 = csum_kernel with the 6LoWPAN NHC gates; 0 before the first launch. */
+uint32_t smol_csum_tool_last_launch(void);
 
 #ifdef __cplusplus
 }

@@ -38,7 +38,7 @@ TOOL_SYMBOLS = [
     "smol_csum_tool_set_xcd_remap", "smol_csum_tool_set_launch_records",
     "smol_csum_tool_field_probe",
     "smol_csum_tool_field_probe_list",
-    "smol_csum_tool_kernel_name",
+    "smol_csum_tool_kernel_name", "smol_csum_tool_last_launch",
 ]
 
 
@@ -151,6 +151,8 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_tool_auto_shape.restype = i32
     L.smol_csum_tool_kernel_name.argtypes = [vp, i32, i32]
     L.smol_csum_tool_kernel_name.restype = ctypes.c_char_p
+    L.smol_csum_tool_last_launch.argtypes = []
+    L.smol_csum_tool_last_launch.restype = u32
     _LIB = L
     return L
 

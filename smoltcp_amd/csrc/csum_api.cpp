@@ -218,12 +218,12 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         return SMOL_OK;
     }
     if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
-        // default: variant 17 (csum_copy.hip: body chunks = one source load + shift + sum + store,
-        // window and edge chunks generic) at its default shape (16 x 4, round 1 carrying 32 body
-        // chunks): C2copy 0.772-0.853 ms (variant 16) -> 0.689 ms (tools/exp_copy.py, MI355X).
-        // Variants 1 / 8 / 11 / 16 stay selectable.
+        // default: variant 21 (csum_copy.hip: variant 17's body chunks = one source load + shift +
+        // sum + store, with the first body round's loads issued ahead of round 1's stores) at its
+        // default shape (16 x 4): C2copy 0.772-0.853 ms (variant 16) -> 0.692 ms (17) -> 0.678 ms
+        // (21; tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 / 17 stay selectable.
         const int cv = ctx->variant;
-        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 21) ? cv : 17;
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17) ? cv : 21;
         const int cshape = ctx->shape >= 0 ? ctx->shape : ((var == 17 || var == 21) ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
@@ -517,5 +517,7 @@ const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int h
     const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY);
     return tile ? "csum_tile_kernel" : "csum_kernel";
 }
+
+uint32_t smol_csum_tool_last_launch(void) { return g_last_launch.load(std::memory_order_relaxed); }
 
 }  // extern "C"

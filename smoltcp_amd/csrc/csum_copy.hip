@@ -316,6 +316,7 @@ hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
+    note_launch(KERN_COPY, LBS ? 21 : 17, G, U);
     hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB, LBS>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
@@ -348,7 +349,10 @@ hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hip
     return p.desc == nullptr ? launch_copy2<true>(shape, p, max_blocks, s) : launch_copy2<false>(shape, p, max_blocks, s);
 }
 
-// variant 21: variant 17's default shapes with the first body round's loads ahead of round 1's stores
+// variant 21 (the copy-emit default): variant 17's default shapes with the first body round's loads
+// ahead of round 1's stores.  MI355X, C2copy, interleaved rounds on one box (tools/exp_copy.py,
+// profiles/r04_experiments/copy_emit_lbs.jsonl): 16 x 4 x 1 x 2 0.678 ms against variant 17's 0.692;
+// 16 x 5 x 1 x 1 0.711; also measured and not kept: 16 x 3 x 1 x 3 0.690, 16 x 3 x 1 x 2 0.728.
 hipError_t launch_copy_v21(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const bool im = p.desc == nullptr;
     if (shape == CFG_G16U6)

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/smolcsum.h"
 
 namespace smolcsum {
@@ -80,6 +82,16 @@ __device__ inline uint64_t logical_block(uint32_t xcd_remap) {
                             : xcd_chunk(blockIdx.x, gridDim.x, xcd_remap);
 }
 #endif
+
+// The kernel instantiation of the process's last checksum launch, packed kernel << 24 | variant << 16
+// | G << 8 | U (smol_csum_tool_last_launch): tests check that a forced variant runs the kernel it
+// names rather than a dispatch fallback.
+enum { KERN_WALK = 1, KERN_TILE = 2, KERN_COPY = 3, KERN_WALK_NHC = 4 };
+inline std::atomic<uint32_t> g_last_launch{0};
+inline void note_launch(uint32_t kern, uint32_t var, uint32_t g, uint32_t u) {
+    g_last_launch.store(kern << 24 | (var & 0xffu) << 16 | (g & 0xffu) << 8 | (u & 0xffu),
+                        std::memory_order_relaxed);
+}
 
 // A dispatch may hold at most 2^32 - 1 work-items: 256-thread grids are capped at 2^24 - 1 blocks
 // (every kernel loops with a grid stride, so a capped grid still covers the whole batch; C5's 2^27

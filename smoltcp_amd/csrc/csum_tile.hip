@@ -388,6 +388,7 @@ static hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t 
     (void)kern;
     const uint64_t cap = p.num_cu == 0 ? max_blocks : (uint64_t)0x7fffffff;
     const uint32_t blocks = grid_blocks(want, cap);
+    note_launch(KERN_TILE, VAR, G, U);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }

@@ -1158,6 +1158,7 @@ hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
+    note_launch(NHC ? KERN_WALK_NHC : KERN_WALK, VAR, G, U);
     hipLaunchKernelGGL((csum_kernel<G, U, MODE, IMPLICIT, VAR, NHC>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
@@ -1206,6 +1207,24 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
         case 29:
             if constexpr (MODE == MODE_EMIT && IMPLICIT) return launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s);
             return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
+        case 23:
+        case 24:
+        case 25:
+        case 26:
+        case 27:
+        case 28:
+            if constexpr (MODE == MODE_EMIT) {
+                switch (var) {
+                    case 23: return launch_seg_shape<IMPLICIT, 23>(shape, p, max_blocks, s);
+                    case 24: return launch_seg_shape<IMPLICIT, 24>(shape, p, max_blocks, s);
+                    case 25: return launch_seg_shape<IMPLICIT, 25>(shape, p, max_blocks, s);
+                    case 26: return launch_seg_shape<IMPLICIT, 26>(shape, p, max_blocks, s);
+                    case 27: return launch_seg_shape<IMPLICIT, 27>(shape, p, max_blocks, s);
+                    default: return launch_seg_shape<IMPLICIT, 28>(shape, p, max_blocks, s);
+                }
+            }
+            return var >= 26 ? launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s)
+                             : launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 9:
         case 10:
             if constexpr (MODE == MODE_EMIT && IMPLICIT) {

@@ -319,6 +319,17 @@ class ChecksumEngine:
         code = {"data": 0, "emit": 1, "verify": 2, "copy_emit": 3}[op]
         return lib().smol_csum_tool_kernel_name(self._h, code, int(bool(has_desc))).decode()
 
+    @staticmethod
+    def last_launch() -> dict:
+        """The kernel instantiation of the process's last checksum launch: {"kernel": "csum_kernel" |
+        "csum_tile_kernel" | "copy_kernel" | "csum_kernel_nhc", "variant": VAR, "G": lanes per record,
+        "U": chunks per lane per step} (None before the first launch)."""
+        w = int(lib().smol_csum_tool_last_launch())
+        names = {1: "csum_kernel", 2: "csum_tile_kernel", 3: "copy_kernel", 4: "csum_kernel_nhc"}
+        if not w >> 24:
+            return None
+        return {"kernel": names.get(w >> 24, "?"), "variant": (w >> 16) & 0xff, "G": (w >> 8) & 0xff, "U": w & 0xff}
+
     def set_xcd_remap(self, on: int):
         """1 / 0: force the XCD-contiguous block order on / off; K >= 2: runs of K workgroups per XCD
         turn; -1: the library's choice."""

@@ -110,11 +110,15 @@ def _run(eng, recs, copies_spec, caps=(0, 0, 0, 0, 0), shape=-1, fixed_stride=No
             batch = E.Batch.from_records(offs, lens, kinds, "cuda:0")
             dv = d
         eng.copy_emit(dv, batch, dsrc, dcp, caps=caps, status=st)
+        launched = eng.last_launch()
         got = d.cpu().numpy()
     finally:
         eng.set_shape(-1)
         eng.set_variant(-1)
         eng.set_max_blocks(0)
+    if n:  # the forced variant ran its own kernel (default: copy_kernel variant 21)
+        want = ("csum_kernel", variant) if variant in (1, 8, 11, 16) else ("copy_kernel", 17 if variant == 17 else 21)
+        assert (launched["kernel"], launched["variant"]) == want, (variant, launched)
     diff = np.nonzero(got != ref)[0]
     assert diff.size == 0, f"bytes differ at {diff[:8]} (got {got[diff[:8]]} want {ref[diff[:8]]})"
     assert np.array_equal(st.cpu().numpy(), ref_st)

@@ -463,11 +463,14 @@ def _emit_case(eng, host, off, n, stride, L, kind, caps, variant, shape=-1, bloc
     eng.set_max_blocks(blocks)
     try:
         eng.emit(d, batch, caps=caps, status=st)
+        launched = eng.last_launch()
         got = full.cpu().numpy()
     finally:
         eng.set_variant(-1)
         eng.set_shape(-1)
         eng.set_max_blocks(0)
+    if variant >= 0:
+        assert _kv(launched) == _expected_launch(variant, "emit", False), (variant, launched)
     ref = host.copy()
     sub = ref[off:].copy()
     ref_st = oracle.batch_emit(sub, None, n, stride, L, kind, caps)
@@ -551,6 +554,25 @@ def test_emit_large_batch(eng):
         _emit_case(eng, host, off, n, stride, L, E.KIND_IP, CAPS_DEFAULT, -1)
 
 
+def _kv(launched):
+    return (launched["kernel"], launched["variant"])
+
+
+def _expected_launch(variant, op, has_desc):
+    """The kernel instantiation a forced `variant` must run (csum_walk.h launch_walk, csum_api.cpp
+    run): (kernel, VAR template argument)."""
+    if variant in (3, 4, 7):
+        return ("csum_tile_kernel", {3: 0, 4: 1, 7: 2}[variant])
+    emit_fixed = op == "emit" and not has_desc
+    if variant in (9, 10, 29):
+        return ("csum_kernel", variant if emit_fixed else 5)
+    if 23 <= variant <= 28:
+        if op == "emit":
+            return ("csum_kernel", variant)
+        return ("csum_kernel", 13 if variant >= 26 else 5)
+    return ("csum_kernel", variant)
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 13, 19, 23, 24, 25, 26, 27, 28, 29])
 def test_variants_fixed_stride(eng, variant):
     """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
@@ -577,14 +599,18 @@ def test_variants_fixed_stride(eng, variant):
                     eng.set_max_blocks(blocks)
                     try:
                         st = eng.verify(buf, batch).cpu().numpy()
+                        launched_v = eng.last_launch()
                         d2 = buf.clone()
                         est = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
                         eng.emit(d2, batch, status=est)
+                        launched_e = eng.last_launch()
                         got = d2.cpu().numpy()
                     finally:
                         eng.set_variant(-1)
                         eng.set_shape(-1)
                         eng.set_max_blocks(0)
+                    assert _kv(launched_v) == _expected_launch(variant, "verify", False), launched_v
+                    assert _kv(launched_e) == _expected_launch(variant, "emit", False), launched_e
                     assert np.array_equal(st, ref_v), (variant, L, stride, shape, blocks)
                     assert np.array_equal(got, ref_e), (variant, L, stride, shape, blocks)
                     assert np.array_equal(est.cpu().numpy(), ref_es)

@@ -80,11 +80,14 @@ def _desc_case(eng, host, offs, lens, kinds, flags=0, variants=SEG_VARIANTS, blo
                 eng.set_max_blocks(blocks)
                 try:
                     eng.emit(d, batch, status=st)
+                    launched = eng.last_launch()
                     got = d.cpu().numpy()
                 finally:
                     eng.set_variant(-1)
                     eng.set_shape(-1)
                     eng.set_max_blocks(0)
+                if variant >= 0:
+                    assert (launched["kernel"], launched["variant"]) == ("csum_kernel", variant), launched
                 diff = np.nonzero(got != ref)[0]
                 assert diff.size == 0, (variant, shape, blocks, diff[:8])
                 assert np.array_equal(st.cpu().numpy(), ref_st), (variant, shape, blocks)
