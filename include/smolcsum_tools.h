@@ -101,6 +101,11 @@ int smol_csum_tool_field_probe(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t by
  * offset with the values it holds (the store shape of whole-segment emit; nothing changes). */
 int smol_csum_tool_field_probe_list(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
                                     const uint32_t* d_piece_first, int flags, void* stream);
+/* A separate store pass (experiments: what emit's field stores cost outside the read stream):
+ * for i < n, the big-endian 2-byte value d_vals[i] at byte offset d_addrs[i] of the buffer, one
+ * thread per store.  `flags` bit 0: non-temporal stores. */
+int smol_csum_tool_field_scatter(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
+                                 const uint16_t* d_vals, uint64_t n, int flags, void* stream);
 /* The launch shape the library picks for a verify over an implicit batch of `len`-byte records. */
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc);
 

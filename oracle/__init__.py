@@ -40,7 +40,11 @@ class CapsC(ctypes.Structure):
 
 def build() -> str:
     """Compile liboracle.so with the committed Makefile; returns its path."""
-    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    import fcntl
+
+    with open(os.path.join(_HERE, ".make.lock"), "w") as lk:  # one make at a time (pytest-xdist workers)
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return os.path.join(_HERE, "liboracle.so")
 
 

@@ -37,7 +37,7 @@ TOOL_SYMBOLS = [
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
     "smol_csum_tool_set_xcd_remap", "smol_csum_tool_set_launch_records",
     "smol_csum_tool_field_probe",
-    "smol_csum_tool_field_probe_list",
+    "smol_csum_tool_field_probe_list", "smol_csum_tool_field_scatter",
     "smol_csum_tool_kernel_name", "smol_csum_tool_last_launch",
 ]
 
@@ -147,6 +147,8 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_tool_field_probe.restype = i32
     L.smol_csum_tool_field_probe_list.argtypes = [vp, vp, u64, vp, vp, ctypes.c_int, vp]
     L.smol_csum_tool_field_probe_list.restype = i32
+    L.smol_csum_tool_field_scatter.argtypes = [vp, vp, u64, vp, vp, u64, ctypes.c_int, vp]
+    L.smol_csum_tool_field_scatter.restype = i32
     L.smol_csum_tool_auto_shape.argtypes = [u32, i32]
     L.smol_csum_tool_auto_shape.restype = i32
     L.smol_csum_tool_kernel_name.argtypes = [vp, i32, i32]

@@ -136,6 +136,8 @@ hipError_t launch_stream_read(const uint8_t* buf, uint64_t bytes, uint32_t* sink
                               hipStream_t s);
 hipError_t launch_field_probe(uint8_t* buf, uint64_t bytes, uint64_t stride, uint32_t f1, uint32_t f2,
                               uint32_t max_blocks, hipStream_t s);
+hipError_t launch_field_scatter(uint8_t* buf, uint64_t bytes, const uint64_t* addrs, const uint16_t* vals, uint64_t n,
+                                int nt, hipStream_t s);
 hipError_t launch_field_probe_list(uint8_t* buf, uint64_t bytes, const uint64_t* addrs, const uint32_t* first,
                                    int seg64, uint32_t max_blocks, hipStream_t s);
 

@@ -360,6 +360,31 @@ hipError_t launch_field_probe_list(uint8_t* buf, uint64_t bytes, const uint64_t*
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void field_scatter_kernel(uint8_t* buf, uint64_t bytes, const uint64_t* addrs,
+                                                            const uint16_t* vals, uint64_t n, int nt) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = addrs[i];
+    const uint32_t v = vals[i];
+    if (a + 2 > bytes) return;
+    __attribute__((address_space(1))) uint8_t* g = (__attribute__((address_space(1))) uint8_t*)(buf + a);
+    if (nt) {
+        __builtin_nontemporal_store((uint8_t)(v >> 8), g);
+        __builtin_nontemporal_store((uint8_t)v, g + 1);
+    } else {
+        g[0] = (uint8_t)(v >> 8);
+        g[1] = (uint8_t)v;
+    }
+}
+
+hipError_t launch_field_scatter(uint8_t* buf, uint64_t bytes, const uint64_t* addrs, const uint16_t* vals, uint64_t n,
+                                int nt, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(field_scatter_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, buf, bytes, addrs,
+                       vals, n, nt);
+    return hipGetLastError();
+}
+
 hipError_t launch_field_probe(uint8_t* buf, uint64_t bytes, uint64_t stride, uint32_t f1, uint32_t f2,
                               uint32_t max_blocks, hipStream_t s) {
     hipLaunchKernelGGL(field_probe_kernel, dim3(max_blocks), dim3(256), 0, s, buf, bytes / 16, stride, f1, f2);

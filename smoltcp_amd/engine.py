@@ -305,6 +305,13 @@ class ChecksumEngine:
                                                     self._stream(stream)),
               "smol_csum_tool_field_probe_list")
 
+    def field_scatter(self, buf, addrs, vals, nt: bool = False, stream=None):
+        """A separate store pass (tooling, smol_csum_tool_field_scatter): the big-endian u16 `vals[i]`
+        at byte offset `addrs[i]` (device int64 / uint16-as-int16 tensors) of `buf`."""
+        check(lib().smol_csum_tool_field_scatter(self._h, buf.data_ptr(), buf.numel(), addrs.data_ptr(),
+                                                 vals.data_ptr(), int(addrs.numel()), int(bool(nt)),
+                                                 self._stream(stream)), "smol_csum_tool_field_scatter")
+
     def set_shape(self, shape: int):
         check(lib().smol_csum_tool_set_shape(self._h, int(shape)), "smol_csum_tool_set_shape")
 

@@ -20,7 +20,12 @@ BIN = os.path.join(CPP, "test_host_mirror")
 
 @pytest.fixture(scope="module")
 def binary():
-    subprocess.run(["make", "-s", "-C", CPP], check=True)
+    # one make at a time: pytest-xdist workers may each build this module's binary
+    import fcntl
+
+    with open(os.path.join(CPP, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", CPP], check=True)
     return BIN
 
 

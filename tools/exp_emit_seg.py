@@ -2,7 +2,7 @@
 """Experiment: emit variants (whole 64-B field segments: 19, 23-27; 2-B stores: 5, 13; the tile
 kernel: 7) on C2 / C3 / C4 at steady clocks, interleaved rounds on one box; every variant must leave
 the same bytes as the first one listed.
-Usage: [VARS=5,19,23] [VARS_c3=7,26,27] [K=30] exp_emit_seg.py [c2,c4,c3]"""
+Usage: [VARS=5,19,23] [VARS_c3=7,26,27] [K=30] [NOCHECK=34 (variants allowed to differ)] exp_emit_seg.py [c2,c4,c3]"""
 import json
 import os
 import sys
@@ -39,7 +39,7 @@ def main():
             else:
                 same = bool(torch.equal(ref, t))
                 print(json.dumps({"cfg": c, "variant": v, "identical_to_first": same}), flush=True)
-                if not same:
+                if not same and str(v) not in os.environ.get("NOCHECK", "").split(","):
                     raise SystemExit(f"{c}: variant {v} differs from variant {vars_of(c)[0]}")
                 del t
         del ref
