@@ -1,0 +1,66 @@
+"""The measurement tools of include/smolcsum_tools.h that experiments rely on: the field-scatter pass
+(tools/exp_scatter.py) and the launched-kernel record (smol_csum_tool_last_launch) over every
+kernel family."""
+import numpy as np
+import pytest
+import torch
+
+from smoltcp_amd import engine as E
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = E.ChecksumEngine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("nt", [False, True])
+def test_field_scatter(eng, nt):
+    """Every listed 2-B big-endian value lands at its offset (odd and even offsets, the buffer's
+    last two bytes); every other byte is untouched; offsets past the buffer are skipped."""
+    rng = np.random.default_rng(3 + nt)
+    size = 1 << 16
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    offs = np.unique(rng.integers(0, size - 1, 3000)).astype(np.int64)
+    offs = offs[np.concatenate([[True], np.diff(offs) >= 2])]  # no two stores overlap
+    offs = np.concatenate([offs[offs < size - 3], [size - 2]])
+    vals = rng.integers(0, 1 << 16, offs.size).astype(np.uint16)
+    ref = host.copy()
+    ref[offs] = (vals >> 8).astype(np.uint8)
+    ref[offs + 1] = (vals & 0xFF).astype(np.uint8)
+    d = torch.from_numpy(host.copy()).cuda()
+    a = torch.from_numpy(np.concatenate([offs, [size - 1, size + 100]])).cuda()  # two past the end
+    v = torch.from_numpy(np.concatenate([vals, [1, 2]]).astype(np.uint16).view(np.int16)).cuda()
+    eng.field_scatter(d, a, v, nt=nt)
+    got = d.cpu().numpy()
+    assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:8]
+
+
+def test_last_launch_families(eng):
+    """The launched-kernel record names the kernel family and the variant each entry point ran."""
+    n, L = 257, 1500
+    buf = torch.zeros(n * L, dtype=torch.uint8, device="cuda:0")
+    b = E.Batch.fixed(n, L, L, E.KIND_IP)
+    eng.synth(buf, b, E.SYNTH_UDP4, seed=1)
+    eng.emit(buf, b)
+    ll = eng.last_launch()
+    assert (ll["kernel"], ll["variant"], ll["G"]) == ("csum_kernel", 29, 8), ll
+    eng.verify(buf, b)
+    ll = eng.last_launch()
+    assert (ll["kernel"], ll["variant"]) == ("csum_kernel", 5), ll
+    offs = np.arange(n, dtype=np.uint64) * L
+    bd = E.Batch.from_records(offs, np.full(n, L, np.uint32), E.KIND_IP, "cuda:0")
+    eng.emit(buf, bd)
+    ll = eng.last_launch()
+    assert (ll["kernel"], ll["variant"]) == ("csum_tile_kernel", 2), ll
+    eng.verify(buf, bd)
+    ll = eng.last_launch()
+    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("csum_kernel", 13, 16, 4), ll
+    src = torch.zeros(n * 1472 + 16, dtype=torch.uint8, device="cuda:0")
+    cp = torch.from_numpy(E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472).view(np.uint8).copy()).cuda()
+    eng.copy_emit(buf, b, src, cp)
+    ll = eng.last_launch()
+    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("copy_kernel", 21, 16, 4), ll
