@@ -1,5 +1,5 @@
 # SQ instruction / cycle counters per kernel of one bench config (one rocprofv3 pass).
-# Usage: gpurun -- 'CFG=c2copy bash tools/gpu_pmc_sq.sh'
+# Usage: gpurun -- 'CFG=c2copy KF=smolcsum bash tools/gpu_pmc_sq.sh'  (KF: kernel-name filter of the summary, default csum_)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
