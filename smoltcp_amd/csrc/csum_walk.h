@@ -325,6 +325,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Store a big-endian u16 at any byte alignment.
 __device__ __forceinline__ void store_be16(gu8 q, uint32_t v) {
+#ifdef SMOL_EXP_NOSTORE  // experiment builds only (tools/gpu_r04_nostore.sh): the value computed, not stored
+    asm volatile("" ::"v"(v), "v"(q));
+    return;
+#endif
     if (((uint64_t)q & 1u) == 0) {
         *(gu16)q = (uint16_t)bswap16(v);
     } else {
@@ -1016,6 +1020,11 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                     wave_lds_sync();
                     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
                     auto seg_store = [&](uint64_t d) {
+#ifdef SMOL_EXP_NOSTORE
+                        u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - base));
+                        asm volatile("" ::"v"(x), "v"(d));
+                        return;
+#endif
                         *(GMEM u32x2*)d = *reinterpret_cast<const u32x2*>(winb + (d - base));
                     };
                     if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
