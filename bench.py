@@ -4,7 +4,9 @@
 Workload (BASELINE.json configs[1], "C2"): per GPU 2^20 IPv4/UDP datagrams of 1500 bytes in HBM
 at a fixed 1500-byte stride.  One step = smol_csum_batch_emit over the TX batch (fill the IPv4
 header and UDP checksums) + smol_csum_batch_verify over the RX batch (the same kind of datagrams,
-already emitted, with 1/64 of them single-bit corrupted as phy::FaultInjector does).  Metric: GiB/s
+already emitted, with 1/64 of them single-bit corrupted as phy::FaultInjector does).  The steps take
+four TX / RX batch pairs in turn (--batches), so that every emit fills a batch whose field lines the
+previous pass did not just write, as a TX path does.  Metric: GiB/s
 checksummed = bytes covered by checksum::data spans (IPv4 header + UDP length) of both passes ÷
 wall time, summed over GPUs (weak scaling: every rank owns its own batch; no collective on the
 data path — only barrier + a max-reduction of the elapsed time for reporting).
@@ -61,6 +63,9 @@ def parse_args(argv=None):
     ap.add_argument("--xcd-remap", type=int, default=-1, help="1/0: force the XCD-contiguous block order (tuning; "
                                                                "-1: the library's choice)")
     ap.add_argument("--launch-records", type=int, default=-1, help="records per kernel launch (tuning; 0: all)")
+    ap.add_argument("--batches", type=int, default=4,
+                    help="TX / RX batch pairs the steps take in turn (1: re-emit one batch; C5 always 1: its one "
+                         "201-GB buffer is emitted and verified in place)")
     ap.add_argument("--probe", action="store_true", help="(kept for old scripts: the probes always run)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch + rendezvous + reporting only, on CPU (gloo), no checksum work")
@@ -121,7 +126,7 @@ def launch_ranks(args, argv) -> int:
 class Workload:
     """Two HBM batches (tx, rx) of one config, generated on the device."""
 
-    def __init__(self, E, eng, cfg: str, n: int, rank: int, dev):
+    def __init__(self, E, eng, cfg: str, n: int, rank: int, dev, batches: int = 1):
         import torch
 
         self.cfg = cfg
@@ -185,6 +190,15 @@ class Workload:
             eng.corrupt(self.rx, self.batch, every=64, seed=seed)
         self.status = torch.empty(self.n, dtype=torch.uint8, device=dev)
         self.est = None
+        # Batch pairs the steps take in turn.  A TX path fills new frames every time (udp.rs:300-308,
+        # tcp.rs:1087-1095): re-emitting one batch lets the ~80 MB of field segments a C2 pass writes
+        # sit dirty in the 256-MB Infinity Cache, where the next pass rewrites them without a DRAM
+        # write (emit 4-9 % faster).  With R pairs, each step emits a batch R steps old.
+        self.txs, self.rxs = [self.tx], [self.rx]
+        if cfg != "c5":
+            for _ in range(max(1, batches) - 1):
+                self.txs.append(self.tx.clone())
+                self.rxs.append(self.rx.clone())
         # emit's floor probe on fixed-stride IPv4 batches: (record stride, field offsets) — the IPv4
         # header checksum and the UDP checksum; C3 / C4 list their fields from the headers (field_addrs)
         self.probe_fields = (1500, 10, 26)
@@ -590,21 +604,26 @@ def main(argv=None):
     eng.set_xcd_remap(args.xcd_remap)
     if args.launch_records >= 0:
         eng.set_launch_records(args.launch_records)
-    wl = Workload(E, eng, args.config, args.n, rank, dev)
+    wl = Workload(E, eng, args.config, args.n, rank, dev, args.batches)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
+    R = len(wl.txs)
+    nstep = [0]
 
-    def step(ev=None):
+    def step(ev=None, same=False):
+        # step i emits TX batch i mod R and verifies RX batch i mod R (same: batch 0 every time)
+        j = 0 if same else nstep[0] % R
+        nstep[0] += 1
         if ev is not None:
             ev[0].record(stream)
         if wl.copy is not None:
-            eng.copy_emit(wl.tx, wl.batch, wl.src, wl.copy, stream=stream)
+            eng.copy_emit(wl.txs[j], wl.batch, wl.src, wl.copy, stream=stream)
         else:
-            eng.emit(wl.tx, wl.batch, stream=stream)
+            eng.emit(wl.txs[j], wl.batch, stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        eng.verify(wl.rx, wl.batch, status=wl.status, stream=stream)
+        eng.verify(wl.rxs[j], wl.batch, status=wl.status, stream=stream)
         if ev is not None:
             ev[2].record(stream)
 
@@ -647,6 +666,23 @@ def main(argv=None):
     emit_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     verify_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
 
+    # Side figure (not the value): the same K instrumented steps re-emitting ONE batch, as the bench
+    # did through round 4.  Its field segments stay dirty in the Infinity Cache between passes, so
+    # its emit is faster than a TX path's.
+    same_batch = None
+    if R > 1:
+        evs1 = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        for i in range(args.steps):
+            step(evs1[i], same=True)
+        torch.cuda.synchronize()
+        e1 = float(np.mean([e[0].elapsed_time(e[1]) for e in evs1]))
+        v1 = float(np.mean([e[1].elapsed_time(e[2]) for e in evs1]))
+        same_batch = {"emit_ms": round(e1, 4), "verify_ms": round(v1, 4),
+                      "emit_fresh_over_same": round(emit_ms / e1, 4),
+                      "what": "K instrumented steps over batch pair 0 only (the round-1..4 bench form), right after "
+                              "the rotating pass: the field segments the previous pass wrote are still dirty in "
+                              "the Infinity Cache"}
+
     # the expected rejections of the last verify (1/64 single-bit flips, or none for C5)
     st = wl.status.cpu().numpy()
     rejected = int(((st & E.ST_ACCEPT) == 0).sum())
@@ -655,7 +691,7 @@ def main(argv=None):
     # Emit's floor (rank 0): the read-only stream probe over the TX buffer, and the same stream plus
     # emit's scattered field stores (smol_csum_tool_field_probe: 2-B stores at the records' field
     # offsets, one store event per field per record): the floor of an emit that stores its fields as
-    # 2-B writes.  Fixed-stride emit (variant 29) writes most IPv4 field segments whole and runs
+    # 2-B writes.  Fixed-stride emit (variant 39) writes most field segments whole and runs
     # under it.
     probe = floor = None
     if rank == 0 and wl.copy is None:
@@ -700,41 +736,8 @@ def main(argv=None):
         floor = {"kernel": "field_probe_kernel", "ms": round(fp_ms, 4), "read_only_ms": round(ro_ms, 4),
                  "what": "the 2-B-store reference: the TX buffer streamed once (best read pattern) + " + where
                          + " (emit's store events as 2-B writes, no parse / gates); fixed-stride emit writes "
-                         "whole 64-B field segments (variant 29) and runs under it; the bytes the probe "
+                         "whole 64-B field segments (variant 39) and runs under it; the bytes the probe "
                          "overwrote are restored"}
-
-    # Fresh batches (rank 0, batches of at most 4 GB): the timed steps re-emit the same TX batch, and
-    # the ~70 MB of field segments one C2 pass writes stay dirty in the 256-MB Infinity Cache, where
-    # the next pass rewrites them; a TX path that emits a new batch every time pays their DRAM writes
-    # (DESIGN.md §5).  Emit over R = 4 batches in turn beside emit over one, interleaved.
-    fresh = None
-    if rank == 0 and wl.copy is None and wl.tx.numel() <= (4 << 30):
-        R = 4
-        txs = [wl.tx] + [wl.tx.clone() for _ in range(R - 1)]
-        torch.cuda.synchronize()
-
-        def emit_loop(bufs, reps):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            for i in range(R):
-                eng.emit(bufs[i % len(bufs)], wl.batch, stream=stream)
-            a.record(stream)
-            for i in range(reps):
-                eng.emit(bufs[i % len(bufs)], wl.batch, stream=stream)
-            b.record(stream)
-            torch.cuda.synchronize()
-            return a.elapsed_time(b) / reps
-
-        same, rot = [], []
-        for _ in range(3):
-            same.append(emit_loop(txs[:1], 4 * R))
-            rot.append(emit_loop(txs, 4 * R))
-        del txs
-        torch.cuda.empty_cache()
-        fresh = {"emit_same_batch_ms": round(float(np.median(same)), 4),
-                 "emit_fresh_batches_ms": round(float(np.median(rot)), 4), "batches": R,
-                 "what": "emit alone over the same TX batch (as in the timed steps) and over 4 batches in turn "
-                         "(every emit a batch its previous pass did not just write): the second pays the DRAM "
-                         "writes of the field segments that the Infinity Cache absorbs in the first"}
 
     unfused = None
     if wl.copy is not None and rank == 0:
@@ -810,7 +813,10 @@ def main(argv=None):
                      "what": "untimed steps before the W warm-up steps until the GPU clocks have ramped "
                              "(steady state: profiles/r03_steps/)"},
             "verify_rejected": rejected,
-            "emit_fresh_batches": fresh,
+            "batches": {"pairs": R, "what": (f"step i emits TX batch i mod {R} and verifies RX batch i mod {R} "
+                                             "(timed steps and kernel timings alike)") if R > 1 else
+                        "one batch (C5: emit and verify in place over one 201-GB buffer)"},
+            "emit_same_batch": same_batch,
             "per_rank": per_rank,
             "cpu_baseline": cpu,
             "parity_sample": parity,

@@ -103,7 +103,8 @@ int smol_csum_tool_field_probe_list(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64
                                     const uint32_t* d_piece_first, int flags, void* stream);
 /* A separate store pass (experiments: what emit's field stores cost outside the read stream):
  * for i < n, the big-endian 2-byte value d_vals[i] at byte offset d_addrs[i] of the buffer, one
- * thread per store.  `flags` bit 0: non-temporal stores. */
+ * thread per store.  `flags` bit 0: non-temporal stores; bit 1: instead write the whole aligned
+ * 64-byte segment holding the offset (the value repeated: a timing probe, the bytes change). */
 int smol_csum_tool_field_scatter(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
                                  const uint16_t* d_vals, uint64_t n, int flags, void* stream);
 /* The launch shape the library picks for a verify over an implicit batch of `len`-byte records. */
@@ -117,6 +118,11 @@ const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int h
  * kernel << 24 | variant << 16 | G << 8 | U; kernel 1 = csum_kernel, 2 = csum_tile_kernel,
  * 3 = copy_kernel, 4 = csum_kernel with the 6LoWPAN NHC gates; 0 before the first launch. */
 uint32_t smol_csum_tool_last_launch(void);
+
+/* 1 when this build of the library runs kernel variant `variant` (smol_csum_tool_set_variant), else
+ * 0.  The product library carries the defaults and one fallback per operation; the experiments
+ * build (`make -C smoltcp_amd/csrc EXP=1`, libsmolcsum_exp.so) every measured variant. */
+int smol_csum_tool_variant_built(int variant);
 
 #ifdef __cplusplus
 }

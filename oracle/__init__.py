@@ -122,6 +122,8 @@ def _bind(L: ctypes.CDLL) -> ctypes.CDLL:
     L.oracle_icmpv6_fill.restype = None
     L.oracle_icmpv6_min_len.argtypes = [ctypes.c_uint8]
     L.oracle_icmpv6_min_len.restype = ctypes.c_size_t
+    L.oracle_hbh_options_drop.argtypes = [u8p, ctypes.c_size_t]
+    L.oracle_hbh_options_drop.restype = ctypes.c_int
     L.oracle_record_verify.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(CapsC)]
     L.oracle_record_verify.restype = ctypes.c_uint8
     L.oracle_record_emit.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(CapsC)]

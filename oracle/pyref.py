@@ -197,3 +197,46 @@ def nhc_udp_fill(p: bytearray, src: bytes, dst: bytes) -> bool:
     p[0] &= ~4 & 0xFF
     fill_l4(p, 1 + ports, c)
     return True
+
+
+# ---- IPv6 Hop-by-Hop options on receive (an independent, literal restatement) -------------------
+
+IPV6_HBH_MAX_OPTIONS = 4  # build.rs:19
+
+
+def _hbh_options(opt: bytes):
+    """Ipv6HopByHopRepr::parse (ipv6hbh.rs:70-89) over Ipv6OptionsIterator (ipv6option.rs:386-420):
+    the option types it keeps, or None when an option fails to parse."""
+    kept, pos = [], 0
+    while pos < len(opt):
+        rest = opt[pos:]
+        t = rest[0]
+        if t == 0:  # Pad1: check_len passes, buffer_len 1 (:172-174, :323)
+            repr_, size = 0, 1
+        else:
+            if len(rest) == 1:  # check_len: no length byte (:176-178)
+                return None
+            dl = rest[1]
+            if len(rest) < 2 + dl:  # check_len: data past the end (:180-184)
+                return None
+            if t == 5 and dl != 2:  # Repr::parse RouterAlert (:293-300)
+                return None
+            repr_, size = t, 2 + dl
+        if len(kept) == IPV6_HBH_MAX_OPTIONS:  # Vec::push fails: `break` (ipv6hbh.rs:82-85)
+            break
+        kept.append(repr_)
+        pos += size
+    return kept
+
+
+def hbh_options_drop(opt: bytes) -> bool:
+    """process_hopbyhop (src/iface/interface/ipv6.rs:282-313): True when the packet is dropped."""
+    kept = _hbh_options(bytes(opt))
+    if kept is None:  # check!(Ipv6HopByHopRepr::parse(..))
+        return True
+    for t in kept:
+        if t in (0, 1, 5):  # Pad1, PadN, RouterAlert
+            continue
+        if t & 0xC0:  # Ipv6OptionFailureType::from(type): Discard / DiscardSendAll / DiscardSendUnicast
+            return True
+    return False

@@ -12,6 +12,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SMOLCSUM_LIB: an alternative build of the same library (A/B experiments only)
 LIB_PATH = os.environ.get("SMOLCSUM_LIB") or os.path.join(_HERE, "libsmolcsum.so")
+# The experiments build (`make -C smoltcp_amd/csrc EXP=1`): the product library plus the measured
+# kernel variants that are not defaults (tools/ and the variant tests load it when it exists).
+EXP_LIB_PATH = os.path.join(_HERE, "libsmolcsum_exp.so")
 
 SMOL_OK, SMOL_EINVAL, SMOL_ENODEV, SMOL_EHIP, SMOL_ERANGE, SMOL_ENOMEM = 0, -1, -2, -3, -4, -5
 ERROR_NAMES = {
@@ -37,7 +40,7 @@ TOOL_SYMBOLS = [
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
     "smol_csum_tool_set_xcd_remap", "smol_csum_tool_set_launch_records",
     "smol_csum_tool_field_probe",
-    "smol_csum_tool_field_probe_list", "smol_csum_tool_field_scatter",
+    "smol_csum_tool_field_probe_list", "smol_csum_tool_field_scatter", "smol_csum_tool_variant_built",
     "smol_csum_tool_kernel_name", "smol_csum_tool_last_launch",
 ]
 
@@ -76,19 +79,20 @@ class BatchC(ctypes.Structure):
     ]
 
 
-_LIB = None
+_LIBS = {}
 
 
-def lib() -> ctypes.CDLL:
-    """Load libsmolcsum.so (raises if it is absent: there is no CPU fallback)."""
-    global _LIB
-    if _LIB is not None:
-        return _LIB
-    if not os.path.exists(LIB_PATH):
+def lib(path: str | None = None) -> ctypes.CDLL:
+    """Load libsmolcsum.so, or the build at `path` (raises if it is absent: there is no CPU
+    fallback)."""
+    path = path or LIB_PATH
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, u8, u16, u32, u64 = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64
     sz, i32 = ctypes.c_size_t, ctypes.c_int
     L.smol_csum_data.argtypes = [vp, sz]
@@ -155,11 +159,13 @@ def lib() -> ctypes.CDLL:
     L.smol_csum_tool_kernel_name.restype = ctypes.c_char_p
     L.smol_csum_tool_last_launch.argtypes = []
     L.smol_csum_tool_last_launch.restype = u32
-    _LIB = L
+    L.smol_csum_tool_variant_built.argtypes = [i32]
+    L.smol_csum_tool_variant_built.restype = i32
+    _LIBS[path] = L
     return L
 
 
-def check(rc: int, what: str) -> None:
+def check(rc: int, what: str, L: ctypes.CDLL | None = None) -> None:
     if rc != SMOL_OK:
-        detail = lib().smol_csum_last_error().decode(errors="replace") if rc == SMOL_EHIP else ""
+        detail = (L or lib()).smol_csum_last_error().decode(errors="replace") if rc == SMOL_EHIP else ""
         raise SmolError(rc, what, detail)

@@ -94,8 +94,11 @@ int walk_variant(int mode, bool has_desc) {
     // fixed-stride emit: variant 5 with the fields' 64-B segments written whole where no neighbour's
     // field shares them (C2 emit 0.305 -> 0.294 ms, tools/exp_emit_seg.py), skipped on wavefronts
     // without an IPv4 record (variant 29: C2 0.2891-0.2894 vs 19's 0.2907-0.2913 ms, C4 0.2649-0.2658
-    // vs 0.2654-0.2666 ms, interleaved on one box, profiles/r04_experiments/)
-    if (!has_desc) return mode == MODE_EMIT ? 29 : 5;
+    // vs 0.2654-0.2666 ms, interleaved on one box, profiles/r04_experiments/).  Round 5: variant 39
+    // = 29, and on a wavefront without an IPv4 record whole segments for IPv6 records too, decided
+    // by one ballot (bench lines over rotating batches, interleaved on one box,
+    // profiles/r05_experiments/emit_variants_bench.txt: C4 5151-5157 -> 5237-5253 GiB/s, C2 equal)
+    if (!has_desc) return mode == MODE_EMIT ? 39 : 5;
     return mode == MODE_EMIT ? 1 : mode == MODE_VERIFY ? 13 : 5;
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
@@ -119,12 +122,32 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
-    if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29) return 5;
+    if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
 
+// The kernel variants this build runs (smol_csum_tool_variant_built).  The product library: the
+// defaults (walk 5 / 13 / 39, tile 7, copy 21) and one fallback each (copy 17; walk 5 and 13 serve
+// each other).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
+bool variant_built(int v) {
+    switch (v) {
+        case -1: case 5: case 7: case 13: case 17: case 21: case 39: return true;
+        default: break;
+    }
+#ifdef SMOL_EXP
+    const int b = v >= 64 ? v - 64 : v;
+    if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39);
+    return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
+           (v >= 31 && v <= 38);
+#else
+    return false;
+#endif
+}
+
 bool line_grid(int variant) {
+    if (variant >= 64) variant -= 64;  // experiment variants without stores
+    if (variant >= 31 && variant <= 39) return true;
     return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 19 ||
            (variant >= 23 && variant <= 29);
 }
@@ -440,8 +463,10 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape) {
     return SMOL_OK;
 }
 
+int smol_csum_tool_variant_built(int variant) { return variant_built(variant) ? 1 : 0; }
+
 int smol_csum_tool_set_variant(smol_csum_ctx_t* ctx, int variant) {
-    if (!ctx || variant < -1 || variant > 29) return SMOL_EINVAL;
+    if (!ctx || !variant_built(variant)) return SMOL_EINVAL;
     ctx->variant = variant;
     return SMOL_OK;
 }

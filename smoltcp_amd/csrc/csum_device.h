@@ -94,13 +94,42 @@ __host__ __device__ __forceinline__ uint32_t icmpv6_min_len(uint32_t t) {
     }
 }
 
+// Whether the iface drops a received packet on the options of its Hop-by-Hop header, record bytes
+// [pos, end) (process_hopbyhop, src/iface/interface/ipv6.rs:282-313):
+//   Ipv6HopByHopRepr::parse (ipv6hbh.rs:70-89) fails on an option that fails Ipv6Option::check_len
+//   (ipv6option.rs:158-182: a lone non-Pad1 byte, or data past the end) or Repr::parse (:286-320:
+//   RouterAlert whose data length is not 2); its Vec holds IPV6_HBH_MAX_OPTIONS = 4 options
+//   (build.rs:19), so the 5th option is parsed and then ends the walk;
+//   the iface drops on any of those 4 that is not Pad1 / PadN / RouterAlert and whose type's top two
+//   bits ask for a discard (Ipv6OptionFailureType, ipv6option.rs:71-77; Rpl 0x63 is Unknown without
+//   the proto-rpl feature).
+// Receive only: emit never parses the options.  Rare (one leading Hop-by-Hop header): <= 5 options.
+template <class RD>
+__device__ __forceinline__ bool hbh_options_drop(const RD& rd, uint32_t pos, uint32_t end) {
+    for (int i = 0; i < 5 && pos < end; ++i) {
+        const uint32_t t = rd(pos);
+        if (t == 0) {  // Pad1
+            pos += 1;
+            continue;
+        }
+        if (end - pos == 1) return true;
+        const uint32_t dl = rd(pos + 1);
+        if (end - pos < 2 + dl) return true;
+        if (t == 5 && dl != 2) return true;
+        if (i < 4 && t != 1 && t != 5 && (t & 0xc0u)) return true;
+        pos += 2 + dl;
+    }
+    return false;
+}
+
 // Record geometry: how smoltcp's iface reaches the checksum gates.  Mirrors, check for check,
 //   Ethernet  src/iface/interface/ethernet.rs:4-46
 //   IPv4      Ipv4Packet::check_len src/wire/ipv4.rs:241-256, version gate :549-551, fragments
 //             src/iface/interface/ipv4.rs:110-146
 //   IPv6      Ipv6Packet::check_len src/wire/ipv6.rs:400-407, one leading Hop-by-Hop header
 //             src/iface/interface/ipv6.rs:205-211,300-303 (Ipv6ExtHeader::check_len,
-//             src/wire/ipv6ext_header.rs:55-69), next header dispatch :323-366
+//             src/wire/ipv6ext_header.rs:55-69; verify: its options, hbh_options_drop), next header
+//             dispatch :323-366
 //   L4        UdpPacket::check_len udp.rs:57-69, TcpPacket::check_len tcp.rs:155-167 (verify: and the
 //             port tests of UdpRepr::parse udp.rs:246-248 / TcpRepr::parse tcp.rs:910-915),
 //             Icmpv4Packet::check_len icmpv4.rs:207-214, IgmpPacket::check_len igmp.rs:73-80,
@@ -198,6 +227,7 @@ __device__ __forceinline__ Geom parse_geometry(const RD& rd, uint32_t len, uint3
             if (rem < 8) { g.st = SMOL_ST_MALFORMED; return g; }
             const uint32_t hbh = (rd(cur + 1) + 1) * 8;
             if (rem < hbh) { g.st = SMOL_ST_MALFORMED; return g; }
+            if (!emit && hbh_options_drop(rd, cur + 2, cur + hbh)) { g.st = SMOL_ST_MALFORMED; return g; }
             nh = rd(cur);
             cur += hbh;
             rem -= hbh;

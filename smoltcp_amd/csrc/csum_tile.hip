@@ -408,19 +408,25 @@ static hipError_t launch_shape(int shape, const KParams& p, uint32_t max_blocks,
     }
 }
 
+// var 2 (variant 7: nt loads on the line grid) is the product's; 0 / 1 (variants 3 / 4: nt / plain
+// loads on the 16-B grid) are in the experiments build only (SMOL_EXP).
 template <int MODE, int TILE>
 static hipError_t launch_mode(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const bool implicit = p.desc == nullptr;
-    if (var == 1) {
-        return implicit ? launch_shape<MODE, true, 1, TILE>(shape, p, max_blocks, s)
-                        : launch_shape<MODE, false, 1, TILE>(shape, p, max_blocks, s);
-    }
     if (var == 2) {
         return implicit ? launch_shape<MODE, true, 2, TILE>(shape, p, max_blocks, s)
                         : launch_shape<MODE, false, 2, TILE>(shape, p, max_blocks, s);
     }
+#ifdef SMOL_EXP
+    if (var == 1) {
+        return implicit ? launch_shape<MODE, true, 1, TILE>(shape, p, max_blocks, s)
+                        : launch_shape<MODE, false, 1, TILE>(shape, p, max_blocks, s);
+    }
     return implicit ? launch_shape<MODE, true, 0, TILE>(shape, p, max_blocks, s)
                     : launch_shape<MODE, false, 0, TILE>(shape, p, max_blocks, s);
+#else
+    return hipErrorInvalidValue;
+#endif
 }
 
 }  // namespace tile

@@ -58,23 +58,40 @@ namespace smolcsum {
 // source bytes from its chunk's first source byte rounded down to 4 (an unaligned 16-byte load), so
 // the funnel is four v_alignbyte and only ONE dword comes from the next lane — and every byte of
 // the record written (WHOLE, see walk_step).  Measured variants that lost are in DESIGN.md §6.
-template <int VAR>
+// Experiment variants (the experiments build, SMOL_EXP, only): emit walks shaped like verify's.
+// 31 = 5 with the geometry in LDS and no shared_from; 32 = 29 with both; 33 = 29 with the geometry
+// in LDS; 34 = 29 without shared_from; 35 = 5 without shared_from; 36 = 5 with the geometry in LDS.
+// VAR | 64 (experiments): the same kernel with every global store of emit compiled out (the values
+// computed and kept live, nothing written; wrong bytes, timing only).
+template <int VAR_>
 struct VarT {
+    static constexpr int VAR = VAR_ & 63;
+    static constexpr bool NOSTORE = (VAR_ & 64) != 0;
+    static constexpr bool GLDS = VAR == 31 || VAR == 32 || VAR == 33 || VAR == 36;
+    // 37 / 38: variant 5 with whole field segments decided by one ballot (BSEG; 38 also IPv6 records)
+    // 39: variant 29 on a wavefront that holds an IPv4 record, 38's ballot decision on one that holds
+    // none (BSEG_NO4: IPv6 records get whole segments too)
+    static constexpr bool BSEG = VAR == 37 || VAR == 38 || VAR == 39;
+    static constexpr bool BSEG6 = VAR == 38 || VAR == 39;
+    static constexpr bool BSEG_NO4 = VAR == 39;
+    static constexpr bool NOSHARE = VAR == 31 || VAR == 32 || VAR == 34 || VAR == 35;
+    static constexpr int BASE = (VAR == 31 || VAR == 35 || VAR == 36 || VAR == 37 || VAR == 38) ? 5
+                                : ((VAR >= 32 && VAR <= 34) || VAR == 39) ? 29 : VAR;
     static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                               (VAR >= 23 && VAR <= 29);
+                               (VAR >= 23 && VAR <= 29) || (VAR >= 31 && VAR <= 39);
     static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 26 && VAR != 27 &&
                                VAR != 28;
     static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                                 (VAR >= 23 && VAR <= 29);
+                                 (VAR >= 23 && VAR <= 29) || (VAR >= 31 && VAR <= 39);
     static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
     static constexpr bool SHUF2 = VAR == 16;
-    static constexpr bool SEGW = VAR == 19 || VAR == 29;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
+    static constexpr bool SEGW = VAR == 19 || BASE == 29;  // variant 5 + whole 64-B field segments (fixed-stride emit, walk_step)
     // SEGOPT bit 0 (29): the segment machinery skipped on wavefronts that hold no IPv4 record (a
     // ballot after the parse: IPv6 records have one field and keep the 2-B store).  (Round 4 also
     // measured the segments stored non-temporal: C2 emit 0.303 against 0.296 ms; removed.)
-    static constexpr int SEGOPT = VAR == 29 ? 1 : 0;
+    static constexpr int SEGOPT = BASE == 29 ? 1 : 0;
     // 23-27 (emit): whole 64-B field segments with the neighbours' record extents published too, so
     // that they serve descriptor batches as well as fixed strides (SEGG); SEGB: the neighbours of the
     // whole workgroup, not only of the wavefront (a workgroup barrier after the parse, natural grid);
@@ -323,12 +340,14 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Store a big-endian u16 at any byte alignment.
+// Store a big-endian u16 at any byte alignment.  NOSTORE (experiment variants only): the value
+// computed and kept live, nothing stored.
+template <bool NOSTORE = false>
 __device__ __forceinline__ void store_be16(gu8 q, uint32_t v) {
-#ifdef SMOL_EXP_NOSTORE  // experiment builds only (tools/gpu_r04_nostore.sh): the value computed, not stored
-    asm volatile("" ::"v"(v), "v"(q));
-    return;
-#endif
+    if constexpr (NOSTORE) {
+        asm volatile("" ::"v"(v), "v"(q));
+        return;
+    }
     if (((uint64_t)q & 1u) == 0) {
         *(gu16)q = (uint16_t)bswap16(v);
     } else {
@@ -404,7 +423,7 @@ __device__ __forceinline__ void emit_fields(const Geom& g, uint32_t f[3]) {
 // SEGP (fixed-stride emit, SEGW): the 64-B segments wsA / wsB (~0: none) go out whole from the
 // window afterwards; a field is patched into the window, and stored to global memory unless both
 // of its bytes lie in those segments.
-template <int G, int MODE, bool NHC, class RD, int WINB = 0, bool SEGP = false>
+template <int G, int MODE, bool NHC, class RD, int WINB = 0, bool SEGP = false, bool NOSTORE = false>
 __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, uint32_t acc, const RD& rd,
                                              const uint8_t* winb, uint32_t head, uint64_t a0, uint64_t r,
                                              int lane, uint8_t* winw = nullptr, uint64_t wsA = ~0ull,
@@ -550,7 +569,7 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
                 const bool cov = (x0 == wsA || x0 == wsB) && (x1 == wsA || x1 == wsB);
                 for (uint32_t i = 0; i < 2; ++i)
                     if (head + f + i < (uint32_t)WINB) winw[head + f + i] = (uint8_t)(i ? v : v >> 8);
-                if (!cov) store_be16(wrec + f, v);
+                if (!cov) store_be16<NOSTORE>(wrec + f, v);
             };
             if (fip != MF_NONE) put(fip, vip);
             if (fin != MF_NONE) put(fin, vin);
@@ -569,9 +588,9 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
             if (fl4 != MF_NONE) put(fl4, vl4);
             if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
         } else if (EMITS) {
-            if (fip != MF_NONE) store_be16(wrec + fip, vip);
-            if (fin != MF_NONE) store_be16(wrec + fin, vin);
-            if (fl4 != MF_NONE) store_be16(wrec + fl4, vl4);
+            if (fip != MF_NONE) store_be16<NOSTORE>(wrec + fip, vip);
+            if (fin != MF_NONE) store_be16<NOSTORE>(wrec + fin, vin);
+            if (fl4 != MF_NONE) store_be16<NOSTORE>(wrec + fl4, vl4);
             if (NHC && nb0 != NO_FIELD) wrec[0] = (uint8_t)nb0;
             if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
         } else {
@@ -598,9 +617,9 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
 // window is used only when record r+1 is the neighbour's one and only record (the natural grid),
 // so that it is filled at the start and never overwritten.  Stride >= 384 keeps that line out of
 // record r's own window.
-template <int G, int MODE, bool IMPLICIT, bool LINE>
+template <int G, int MODE, bool IMPLICIT, bool LINE, bool NOSHARE = false>
 __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, uint64_t a0, int gib, uint64_t ngroups) {
-    constexpr bool SHARE = IMPLICIT && LINE && MODE == MODE_EMIT;
+    constexpr bool SHARE = IMPLICIT && LINE && MODE == MODE_EMIT && !NOSHARE;
     constexpr int GPW = 64 / G;  // groups per wavefront
     if (!SHARE || p.stride < 384 || (gib % GPW) == GPW - 1 || r + 1 >= p.n || r + 1 >= ngroups ||
         r + 1 + ngroups < p.n)
@@ -612,7 +631,7 @@ __device__ __forceinline__ uint64_t shared_from(const KParams& p, uint64_t r, ui
 // and finish the record on its last step.  Returns false when the group has no more work.
 template <int G, int U, int MODE, bool IMPLICIT, bool NT, bool PF, bool SKIPD, bool LINE, bool NHC, int CU = 0,
           bool SHUF = false, bool WHOLE = false, bool SHUF2 = false, bool SEGW = false, bool SEGG = false,
-          bool SEGB = false, bool SEG6 = false, int SEGOPT = 0>
+          bool SEGB = false, bool SEG6 = false, int SEGOPT = 0, int VAR = 0>
 __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MODE == MODE_COPY>& cv,
                                           Regs<U, MODE == MODE_COPY>& nx, int lane, uint64_t ngroups, u32x4* win,
                                           int gib, SegInfo* si = nullptr, SegInfoG* sg = nullptr,
@@ -620,7 +639,11 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     constexpr bool COPY = MODE == MODE_COPY;
     // where the record geometry lives (Walk::g / Walk::gr): registers for emit with the register
     // prefetch, LDS otherwise
-    constexpr bool GREG = MODE == MODE_EMIT && PF;
+    constexpr bool GREG = MODE == MODE_EMIT && PF && !VarT<VAR>::GLDS;
+    constexpr bool NOSHARE = VarT<VAR>::NOSHARE;
+    constexpr bool NOSTORE = VarT<VAR>::NOSTORE;
+    constexpr bool BSEG = VarT<VAR>::BSEG && MODE == MODE_EMIT && IMPLICIT && LINE && !NHC;
+    constexpr bool SEGF = SEGW || BSEG;  // the finish writes the decided segments whole
     constexpr int WIN = Grid<LINE>::WIN;
     constexpr int WIN_CH = Grid<LINE>::WIN_CH;
     static_assert(G * U >= WIN_CH, "step 0 must cover the LDS window");
@@ -636,7 +659,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
     // every record's last step would otherwise issue U loads of the dummy line)
     if (PF && (!SKIPD || have2))
         load_step<G, U, NT, COPY, LINE, CU, SHUF, SHUF2>(nx, rec2, nch2, step2, lane, have2, (uint64_t)p.dummy,
-                                            shared_from<G, MODE, IMPLICIT, LINE>(p, r2, rec2.a0, gib, ngroups));
+                                            shared_from<G, MODE, IMPLICIT, LINE, NOSHARE>(p, r2, rec2.a0, gib, ngroups));
     // descriptor of the record after next (clamped index: an unconditional load)
     RecRef nxt2 = w.nxt;
     {
@@ -765,8 +788,43 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             const Geom& g = GREG ? w.gr : *w.g;
             // the lanes sum [0, span_end): the header part is subtracted at the end
             w.s1 = (g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED)) ? (int)g.span_end : 0;
-            if constexpr (SEGW) w.segA = w.segB = SEG_NONE;
-            if (SEGW && (!(SEGOPT & 1) || __any(g.fam == 4))) {
+            if constexpr (SEGF) w.segA = w.segB = SEG_NONE;
+            // SEGOPT / BSEG_NO4: whether the wavefront holds an IPv4 record (one ballot)
+            const bool any4 = (SEGW && (SEGOPT & 1)) ? __any(g.fam == 4) : true;
+            if (BSEG && (!VarT<VAR>::BSEG_NO4 || !any4)) {
+                // Whole field segments, decided by one ballot.  A segment that starts before the
+                // record also holds record r-1's last bytes; it goes out whole only when r-1 has no
+                // field in its last 64 bytes (then no store of r-1's group can fall into it).  Each
+                // group says so for its own record (ok_tail); with the natural grid every group of
+                // the wavefront is on its one record at step 0, and group gib-1 holds record r-1.
+                // A record whose fields end 64 bytes or more before its end never reaches into r+1
+                // with its own segments.  The first group of a wavefront, a gapped stride and r = 0
+                // keep the 2-B store for a segment that starts before the record.
+                uint32_t f[3], lo = NO_FIELD, hi = 0;
+                emit_fields(g, f);
+                for (int j = 0; j < 3; ++j)
+                    if (f[j] != NO_FIELD) {
+                        lo = f[j] < lo ? f[j] : lo;
+                        hi = f[j] + 2 > hi ? f[j] + 2 : hi;
+                    }
+                const bool ok_tail = hi == 0 || hi + 64 <= w.cur.len;
+                const uint64_t okm = __ballot(lane == 0 && ok_tail);
+                constexpr int GPW = 64 / G;
+                const bool natural = ngroups >= p.n;
+                const bool fam_ok = g.fam == 4 || (VarT<VAR>::BSEG6 && g.fam == 6);
+                if (natural && fam_ok && hi != 0 && ok_tail && w.cur.len < (1u << 29)) {
+                    const uint32_t wl = (uint32_t)(threadIdx.x & 63u);
+                    const bool prev_ok = (gib % GPW) != 0 && w.r > 0 && p.len == p.stride &&
+                                         ((okm >> (wl - (uint32_t)lane - G)) & 1ull);
+                    const int32_t ph = (int32_t)(w.cur.a0 & 63u);
+                    const int32_t rA = ((ph + (int32_t)lo) & ~63) - ph, rB = ((ph + (int32_t)hi - 1) & ~63) - ph;
+                    const int32_t wend = 16 * (int32_t)(w.nch < (uint32_t)WIN_CH ? w.nch : (uint32_t)WIN_CH) - (int32_t)head;
+                    auto whole = [&](int32_t rel) { return rB <= rA + 64 && rel + 64 <= wend && (rel >= 0 || prev_ok); };
+                    if (whole(rA)) w.segA = rA;
+                    if (rB != rA && whole(rB)) w.segB = rB;
+                }
+            }
+            if (SEGW && any4) {
                 // publish every field finish_gates may write (a superset is safe), then decide which
                 // of this record's field segments go out whole (see the finish below)
                 uint32_t f[3], lo = NO_FIELD, hi = 0;
@@ -875,7 +933,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
 
     // ---- sum this step's chunks over [0, s1) (data: [0, len)) ----
     const int s1 = w.s1;
-    const uint64_t lim = shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups);
+    const uint64_t lim = shared_from<G, MODE, IMPLICIT, LINE, NOSHARE>(p, w.r, w.cur.a0, gib, ngroups);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t k = w.step * (G * U) + u * G + lane;
@@ -1003,7 +1061,7 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
             // records and the window holds all of it.  Fields outside such segments are stored as
             // 2-B fields.
             uint64_t wsA = ~0ull, wsB = ~0ull;
-            if constexpr (SEGW) {  // the segments decided after the parse (step 0)
+            if constexpr (SEGF) {  // the segments decided after the parse (step 0)
                 if (w.segA != SEG_NONE) wsA = w.cur.a0 + (int64_t)w.segA;
                 if (w.segB != SEG_NONE) wsB = w.cur.a0 + (int64_t)w.segB;
             }
@@ -1012,20 +1070,17 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                 if (sa != SEG_NONE) wsA = w.cur.a0 + (int64_t)sa;
                 if (sb != SEG_NONE) wsB = w.cur.a0 + (int64_t)sb;
             }
-            finish_gates<G, MODE, NHC, decltype(rd), ((COPY && WHOLE) || SEGW || SEGG) ? WIN : 0, SEGW || SEGG>(
+            finish_gates<G, MODE, NHC, decltype(rd), ((COPY && WHOLE) || SEGF || SEGG) ? WIN : 0, SEGF || SEGG, NOSTORE>(
                 p, GREG ? w.gr : *w.g, w.acc, rd, winb, head, w.cur.a0, r, lane, reinterpret_cast<uint8_t*>(win),
                 wsA, wsB);
-            if constexpr (SEGW || SEGG) {
+            if constexpr (SEGF || SEGG) {
                 if (wsA != ~0ull || wsB != ~0ull) {
                     wave_lds_sync();
                     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
                     auto seg_store = [&](uint64_t d) {
-#ifdef SMOL_EXP_NOSTORE
-                        u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - base));
-                        asm volatile("" ::"v"(x), "v"(d));
-                        return;
-#endif
-                        *(GMEM u32x2*)d = *reinterpret_cast<const u32x2*>(winb + (d - base));
+                        const u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - base));
+                        if constexpr (NOSTORE) asm volatile("" ::"v"(x), "v"(d));
+                        else *(GMEM u32x2*)d = x;
                     };
                     if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
                     if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
@@ -1140,19 +1195,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MinWaves<VA
     if (PF) {
         Regs<U, COPY> vb;
         load_step<G, U, NT, COPY, LINE, CU, SHUF>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
-                                                  shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
+                                                  shared_from<G, MODE, IMPLICIT, LINE, VarT<VAR>::NOSHARE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
             if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6,
-                           VarT<VAR>::SEGOPT>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
+                           VarT<VAR>::SEGOPT, VAR>(p, w, va, vb, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
             if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, CU, SHUF, false, false, SEGW, SEGG, SEGB, SEG6,
-                           VarT<VAR>::SEGOPT>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
+                           VarT<VAR>::SEGOPT, VAR>(p, w, vb, va, lane, ngroups, &win[gib][0], gib, segi, segg, blockwide)) break;
         }
     } else {
         while (true) {
             load_step<G, U, NT, COPY, LINE, 0, SHUF, SHUF2>(va, w.cur, w.nch, w.step, lane, true, (uint64_t)p.dummy,
-                                                            shared_from<G, MODE, IMPLICIT, LINE>(p, w.r, w.cur.a0, gib, ngroups));
-            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF, WHOLE, SHUF2, false, SEGG, SEGB, SEG6>(
+                                                            shared_from<G, MODE, IMPLICIT, LINE, VarT<VAR>::NOSHARE>(p, w.r, w.cur.a0, gib, ngroups));
+            if (!walk_step<G, U, MODE, IMPLICIT, NT, PF, SKIPD, LINE, NHC, 0, SHUF, WHOLE, SHUF2, false, SEGG, SEGB, SEG6, 0, VAR>(
                     p, w, va, va, lane, ngroups, &win[gib][0], gib, nullptr, segg, blockwide)) break;
         }
     }
@@ -1204,16 +1259,48 @@ hipError_t launch_seg_shape(int shape, const KParams& p, uint32_t max_blocks, hi
     }
 }
 
+#ifdef SMOL_EXP
+// Experiment variants of fixed-stride emit (31-38, and | 64 without stores): the two fixed-stride
+// shapes only (other shapes map to the one with the same group size).
+template <int VAR>
+hipError_t launch_emit_exp(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    if (shape == CFG_G8U6) return launch_one<8, 6, MODE_EMIT, true, VAR>(p, max_blocks, s);
+    return launch_one<8, 7, MODE_EMIT, true, VAR>(p, max_blocks, s);
+}
+
+// The experiments build (SMOL_EXP): every walk variant that was measured and is not a default.
 template <int MODE, bool IMPLICIT>
-hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+hipError_t launch_walk_exp(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    if constexpr (MODE == MODE_EMIT && IMPLICIT) {
+        switch (var) {
+            case 31: return launch_emit_exp<31>(shape, p, max_blocks, s);
+            case 32: return launch_emit_exp<32>(shape, p, max_blocks, s);
+            case 33: return launch_emit_exp<33>(shape, p, max_blocks, s);
+            case 34: return launch_emit_exp<34>(shape, p, max_blocks, s);
+            case 35: return launch_emit_exp<35>(shape, p, max_blocks, s);
+            case 36: return launch_emit_exp<36>(shape, p, max_blocks, s);
+            case 37: return launch_emit_exp<37>(shape, p, max_blocks, s);
+            case 38: return launch_emit_exp<38>(shape, p, max_blocks, s);
+            case 64 + 39: return launch_emit_exp<64 + 39>(shape, p, max_blocks, s);
+            case 64 + 5: return launch_emit_exp<64 + 5>(shape, p, max_blocks, s);
+            case 64 + 29: return launch_emit_exp<64 + 29>(shape, p, max_blocks, s);
+            case 64 + 31: return launch_emit_exp<64 + 31>(shape, p, max_blocks, s);
+            case 64 + 32: return launch_emit_exp<64 + 32>(shape, p, max_blocks, s);
+            case 64 + 33: return launch_emit_exp<64 + 33>(shape, p, max_blocks, s);
+            case 64 + 34: return launch_emit_exp<64 + 34>(shape, p, max_blocks, s);
+            case 64 + 35: return launch_emit_exp<64 + 35>(shape, p, max_blocks, s);
+            case 64 + 36: return launch_emit_exp<64 + 36>(shape, p, max_blocks, s);
+            case 64 + 37: return launch_emit_exp<64 + 37>(shape, p, max_blocks, s);
+            case 64 + 38: return launch_emit_exp<64 + 38>(shape, p, max_blocks, s);
+            default: break;
+        }
+    }
     switch (var) {
         case 1: return launch_shape<MODE, IMPLICIT, 1>(shape, p, max_blocks, s);
         case 2: return launch_shape<MODE, IMPLICIT, 2>(shape, p, max_blocks, s);
-        case 5: return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 6: return launch_shape<MODE, IMPLICIT, 6>(shape, p, max_blocks, s);
-        case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
         case 19: return launch_shape<MODE, IMPLICIT, 19>(shape, p, max_blocks, s);
-        case 29:
+        case 29:  // round 4's fixed-stride emit default
             if constexpr (MODE == MODE_EMIT && IMPLICIT) return launch_seg_shape<IMPLICIT, 29>(shape, p, max_blocks, s);
             return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 23:
@@ -1241,7 +1328,32 @@ hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks
                                 : launch_shape<MODE, IMPLICIT, 10>(shape, p, max_blocks, s);
             }
             return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
-        default: return launch_shape<MODE, IMPLICIT, 0>(shape, p, max_blocks, s);
+        case 0: return launch_shape<MODE, IMPLICIT, 0>(shape, p, max_blocks, s);
+        case 31: case 32: case 33: case 34: case 35: case 36: case 37: case 38:
+            return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);  // emit variants: 5 elsewhere
+        default: return hipErrorInvalidValue;
+    }
+}
+#endif
+
+// The product variants (csum_api.cpp variant_built): 5 (line grid, nt loads, register prefetch),
+// 13 (5 without the prefetch) and, for fixed-stride emit, 39 (5 with whole field segments: 29's
+// LDS-published decision on wavefronts with an IPv4 record, one ballot on the others).  Other
+// variants: the experiments build.
+template <int MODE, bool IMPLICIT>
+hipError_t launch_walk(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    switch (var) {
+        case 5: return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
+        case 13: return launch_shape<MODE, IMPLICIT, 13>(shape, p, max_blocks, s);
+        case 39:
+            if constexpr (MODE == MODE_EMIT && IMPLICIT) return launch_seg_shape<IMPLICIT, 39>(shape, p, max_blocks, s);
+            return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
+        default:
+#ifdef SMOL_EXP
+            return launch_walk_exp<MODE, IMPLICIT>(shape, var, p, max_blocks, s);
+#else
+            return hipErrorInvalidValue;
+#endif
     }
 }
 
@@ -1287,15 +1399,20 @@ hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hip
 // variant 21: variant 17 with the first body round's loads ahead of round 1's stores (csum_copy.hip)
 hipError_t launch_copy_v21(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s);
 
+// 17 / 21 (copy_kernel) are the product's; the walk kernel's MODE_COPY variants (1, 8, 11, 16: the
+// round-1 / 2 designs) are in the experiments build only.
 template <bool IMPLICIT>
 hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     switch (var) {
         case 17: return launch_copy_v17(shape, p, max_blocks, s);
         case 21: return launch_copy_v21(shape, p, max_blocks, s);
+#ifdef SMOL_EXP
         case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
         case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);
         case 8: return launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);
-        default: return launch_copy_var<IMPLICIT, 16>(shape, p, max_blocks, s);
+        case 16: return launch_copy_var<IMPLICIT, 16>(shape, p, max_blocks, s);
+#endif
+        default: return hipErrorInvalidValue;
     }
 }
 

@@ -1,8 +1,20 @@
-// Instantiates the fused copy + emit walk kernel (csum_walk.h), and dispatches a batched call to its
-// instantiation.
+// Dispatches a batched call to the walk kernel instantiation for its mode and batch form (and, in the
+// experiments build, instantiates the walk kernel's MODE_COPY variants).
 #include "csum_walk.h"
 
 namespace smolcsum {
+
+// instantiated in csum_walk_{data,emit,verify}_{fixed,desc}.hip and csum_walk_nhc.hip
+extern template hipError_t launch_walk<MODE_DATA, true>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk<MODE_DATA, false>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk<MODE_EMIT, true>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk<MODE_EMIT, false>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk<MODE_VERIFY, true>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk<MODE_VERIFY, false>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk_nhc<MODE_EMIT, true>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk_nhc<MODE_EMIT, false>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk_nhc<MODE_VERIFY, true>(int, int, const KParams&, uint32_t, hipStream_t);
+extern template hipError_t launch_walk_nhc<MODE_VERIFY, false>(int, int, const KParams&, uint32_t, hipStream_t);
 
 hipError_t launch_csum(int mode, int shape, int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
     const bool implicit = p.desc == nullptr;

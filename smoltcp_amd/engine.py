@@ -125,15 +125,17 @@ def _caps(caps) -> Caps:
 class ChecksumEngine:
     """One device context.  Not thread-safe: use one engine per host thread."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, lib_path: Optional[str] = None):
+        """`lib_path`: another build of the library (the experiments build, `_lib.EXP_LIB_PATH`)."""
         self.device = int(device)
+        self._L = lib(lib_path)
         h = ctypes.c_void_p()
-        check(lib().smol_csum_ctx_create(self.device, ctypes.byref(h)), "smol_csum_ctx_create")
+        check(self._L.smol_csum_ctx_create(self.device, ctypes.byref(h)), "smol_csum_ctx_create")
         self._h = h
 
     def close(self):
-        if self._h is not None and self._h.value:
-            lib().smol_csum_ctx_destroy(self._h)
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.smol_csum_ctx_destroy(self._h)
         self._h = None
 
     def __del__(self):
@@ -167,7 +169,7 @@ class ChecksumEngine:
         if out is None:
             out = torch.empty(batch.n, dtype=torch.int16, device=buf.device)
         b = batch.c()
-        check(lib().smol_csum_batch_data(self._h, buf.data_ptr(), ctypes.byref(b), out.data_ptr(),
+        check(self._L.smol_csum_batch_data(self._h, buf.data_ptr(), ctypes.byref(b), out.data_ptr(),
                                          self._stream(stream)), "smol_csum_batch_data")
         return out
 
@@ -176,7 +178,7 @@ class ChecksumEngine:
         self._check_buf(buf, batch)
         b = batch.c()
         c = _caps(caps)
-        check(lib().smol_csum_batch_emit(self._h, buf.data_ptr(), ctypes.byref(b), ctypes.byref(c),
+        check(self._L.smol_csum_batch_emit(self._h, buf.data_ptr(), ctypes.byref(b), ctypes.byref(c),
                                          status.data_ptr() if status is not None else None,
                                          self._stream(stream)), "smol_csum_batch_emit")
         return status
@@ -188,7 +190,7 @@ class ChecksumEngine:
         assert src.is_cuda and copies.is_cuda and copies.numel() >= 16 * batch.n
         b = batch.c()
         c = _caps(caps)
-        check(lib().smol_csum_batch_copy_emit(self._h, buf.data_ptr(), ctypes.byref(b), src.data_ptr(),
+        check(self._L.smol_csum_batch_copy_emit(self._h, buf.data_ptr(), ctypes.byref(b), src.data_ptr(),
                                               copies.data_ptr(), ctypes.byref(c),
                                               status.data_ptr() if status is not None else None,
                                               self._stream(stream)), "smol_csum_batch_copy_emit")
@@ -202,7 +204,7 @@ class ChecksumEngine:
         assert groups.is_cuda and groups.numel() % 16 == 0
         b = batch.c()
         c = _caps(caps)
-        check(lib().smol_csum_batch_emit_frag(self._h, buf.data_ptr(), ctypes.byref(b), groups.data_ptr(),
+        check(self._L.smol_csum_batch_emit_frag(self._h, buf.data_ptr(), ctypes.byref(b), groups.data_ptr(),
                                               groups.numel() // 16, ctypes.byref(c),
                                               status.data_ptr() if status is not None else None,
                                               self._stream(stream)), "smol_csum_batch_emit_frag")
@@ -219,7 +221,7 @@ class ChecksumEngine:
             status = torch.zeros(batch.n, dtype=torch.uint8, device=buf.device)
         b = batch.c()
         c = _caps(caps)
-        check(lib().smol_csum_batch_verify_frag(self._h, buf.data_ptr(), ctypes.byref(b), groups.data_ptr(),
+        check(self._L.smol_csum_batch_verify_frag(self._h, buf.data_ptr(), ctypes.byref(b), groups.data_ptr(),
                                                 groups.numel() // 16, ctypes.byref(c), status.data_ptr(),
                                                 self._stream(stream)), "smol_csum_batch_verify_frag")
         return status
@@ -231,7 +233,7 @@ class ChecksumEngine:
         assert addrs.is_cuda and addrs.numel() >= 32 * batch.n
         b = batch.c()
         c = _caps(caps)
-        check(lib().smol_csum_batch_nhc_udp_emit(self._h, buf.data_ptr(), ctypes.byref(b), addrs.data_ptr(),
+        check(self._L.smol_csum_batch_nhc_udp_emit(self._h, buf.data_ptr(), ctypes.byref(b), addrs.data_ptr(),
                                                  ctypes.byref(c), status.data_ptr() if status is not None else None,
                                                  self._stream(stream)), "smol_csum_batch_nhc_udp_emit")
         return status
@@ -246,7 +248,7 @@ class ChecksumEngine:
             status = torch.empty(batch.n, dtype=torch.uint8, device=buf.device)
         b = batch.c()
         c = _caps(caps)
-        check(lib().smol_csum_batch_nhc_udp_verify(self._h, buf.data_ptr(), ctypes.byref(b), addrs.data_ptr(),
+        check(self._L.smol_csum_batch_nhc_udp_verify(self._h, buf.data_ptr(), ctypes.byref(b), addrs.data_ptr(),
                                                    ctypes.byref(c), status.data_ptr(), self._stream(stream)),
               "smol_csum_batch_nhc_udp_verify")
         return status
@@ -260,7 +262,7 @@ class ChecksumEngine:
             status = torch.empty(batch.n, dtype=torch.uint8, device=buf.device)
         b = batch.c()
         c = _caps(caps)
-        check(lib().smol_csum_batch_verify(self._h, buf.data_ptr(), ctypes.byref(b), ctypes.byref(c),
+        check(self._L.smol_csum_batch_verify(self._h, buf.data_ptr(), ctypes.byref(b), ctypes.byref(c),
                                            status.data_ptr(), self._stream(stream)),
               "smol_csum_batch_verify")
         return status
@@ -269,28 +271,28 @@ class ChecksumEngine:
     def synth(self, buf, batch: Batch, profile: int, seed: int, stream=None):
         self._check_buf(buf, batch)
         b = batch.c()
-        check(lib().smol_csum_tool_synth(self._h, buf.data_ptr(), ctypes.byref(b), int(profile),
+        check(self._L.smol_csum_tool_synth(self._h, buf.data_ptr(), ctypes.byref(b), int(profile),
                                          int(seed) & (2**64 - 1), self._stream(stream)),
               "smol_csum_tool_synth")
 
     def corrupt(self, buf, batch: Batch, every: int, seed: int, stream=None):
         self._check_buf(buf, batch)
         b = batch.c()
-        check(lib().smol_csum_tool_corrupt(self._h, buf.data_ptr(), ctypes.byref(b), int(every),
+        check(self._L.smol_csum_tool_corrupt(self._h, buf.data_ptr(), ctypes.byref(b), int(every),
                                            int(seed) & (2**64 - 1), self._stream(stream)),
               "smol_csum_tool_corrupt")
 
     def stream_read(self, buf, sink, stream=None):
         """Read-only HBM streaming probe over the whole buffer (tooling)."""
         nbytes = buf.numel() // 16 * 16
-        check(lib().smol_csum_tool_stream_read(self._h, buf.data_ptr(), nbytes, sink.data_ptr(),
+        check(self._L.smol_csum_tool_stream_read(self._h, buf.data_ptr(), nbytes, sink.data_ptr(),
                                                self._stream(stream)), "smol_csum_tool_stream_read")
 
     def field_probe(self, buf, stride: int, f1: int, f2: int = 0xFFFFFFFF, stream=None):
         """Emit's floor probe (tooling, smol_csum_tool_field_probe): stream-read the buffer and store
         2 bytes at offsets f1 / f2 of every `stride`-byte record.  Overwrites those bytes."""
         nbytes = buf.numel() // 16 * 16
-        check(lib().smol_csum_tool_field_probe(self._h, buf.data_ptr(), nbytes, int(stride), int(f1), int(f2),
+        check(self._L.smol_csum_tool_field_probe(self._h, buf.data_ptr(), nbytes, int(stride), int(f1), int(f2),
                                                self._stream(stream)), "smol_csum_tool_field_probe")
 
     def field_probe_list(self, buf, addrs, piece_first, seg64: bool = False, stream=None):
@@ -300,38 +302,43 @@ class ChecksumEngine:
         entries).  Overwrites the bytes at those offsets; with `seg64` rewrites the 64-B segments
         holding them whole, with their own values, instead."""
         nbytes = buf.numel() // 16 * 16
-        check(lib().smol_csum_tool_field_probe_list(self._h, buf.data_ptr(), nbytes, addrs.data_ptr(),
+        check(self._L.smol_csum_tool_field_probe_list(self._h, buf.data_ptr(), nbytes, addrs.data_ptr(),
                                                     piece_first.data_ptr(), int(bool(seg64)),
                                                     self._stream(stream)),
               "smol_csum_tool_field_probe_list")
 
-    def field_scatter(self, buf, addrs, vals, nt: bool = False, stream=None):
+    def field_scatter(self, buf, addrs, vals, nt: int = 0, stream=None):
         """A separate store pass (tooling, smol_csum_tool_field_scatter): the big-endian u16 `vals[i]`
-        at byte offset `addrs[i]` (device int64 / uint16-as-int16 tensors) of `buf`."""
-        check(lib().smol_csum_tool_field_scatter(self._h, buf.data_ptr(), buf.numel(), addrs.data_ptr(),
-                                                 vals.data_ptr(), int(addrs.numel()), int(bool(nt)),
+        at byte offset `addrs[i]` (device int64 / uint16-as-int16 tensors) of `buf`.  `nt`: the flags
+        (bit 0 non-temporal stores, bit 1 the whole 64-B segment instead)."""
+        check(self._L.smol_csum_tool_field_scatter(self._h, buf.data_ptr(), buf.numel(), addrs.data_ptr(),
+                                                 vals.data_ptr(), int(addrs.numel()), int(nt),
                                                  self._stream(stream)), "smol_csum_tool_field_scatter")
 
     def set_shape(self, shape: int):
-        check(lib().smol_csum_tool_set_shape(self._h, int(shape)), "smol_csum_tool_set_shape")
+        check(self._L.smol_csum_tool_set_shape(self._h, int(shape)), "smol_csum_tool_set_shape")
 
     def set_variant(self, variant: int):
-        check(lib().smol_csum_tool_set_variant(self._h, int(variant)), "smol_csum_tool_set_variant")
+        check(self._L.smol_csum_tool_set_variant(self._h, int(variant)), "smol_csum_tool_set_variant")
 
     def set_tile(self, records: int):
-        check(lib().smol_csum_tool_set_tile(self._h, int(records)), "smol_csum_tool_set_tile")
+        check(self._L.smol_csum_tool_set_tile(self._h, int(records)), "smol_csum_tool_set_tile")
 
     def kernel_name(self, op: str, has_desc: bool = False) -> str:
         """The kernel an IP-path `op` ("data", "emit", "verify", "copy_emit") launches here."""
         code = {"data": 0, "emit": 1, "verify": 2, "copy_emit": 3}[op]
-        return lib().smol_csum_tool_kernel_name(self._h, code, int(bool(has_desc))).decode()
+        return self._L.smol_csum_tool_kernel_name(self._h, code, int(bool(has_desc))).decode()
 
-    @staticmethod
-    def last_launch() -> dict:
+    def variant_built(self, variant: int) -> bool:
+        """Whether this build of the library runs `variant` (the product library: the defaults and
+        one fallback per operation; the experiments build: every measured variant)."""
+        return bool(self._L.smol_csum_tool_variant_built(int(variant)))
+
+    def last_launch(self) -> dict:
         """The kernel instantiation of the process's last checksum launch: {"kernel": "csum_kernel" |
         "csum_tile_kernel" | "copy_kernel" | "csum_kernel_nhc", "variant": VAR, "G": lanes per record,
         "U": chunks per lane per step} (None before the first launch)."""
-        w = int(lib().smol_csum_tool_last_launch())
+        w = int(self._L.smol_csum_tool_last_launch())
         names = {1: "csum_kernel", 2: "csum_tile_kernel", 3: "copy_kernel", 4: "csum_kernel_nhc"}
         if not w >> 24:
             return None
@@ -340,13 +347,13 @@ class ChecksumEngine:
     def set_xcd_remap(self, on: int):
         """1 / 0: force the XCD-contiguous block order on / off; K >= 2: runs of K workgroups per XCD
         turn; -1: the library's choice."""
-        check(lib().smol_csum_tool_set_xcd_remap(self._h, int(on)), "smol_csum_tool_set_xcd_remap")
+        check(self._L.smol_csum_tool_set_xcd_remap(self._h, int(on)), "smol_csum_tool_set_xcd_remap")
 
     def set_launch_records(self, records: int):
-        check(lib().smol_csum_tool_set_launch_records(self._h, int(records)), "smol_csum_tool_set_launch_records")
+        check(self._L.smol_csum_tool_set_launch_records(self._h, int(records)), "smol_csum_tool_set_launch_records")
 
     def set_max_blocks(self, max_blocks: int):
-        check(lib().smol_csum_tool_set_max_blocks(self._h, int(max_blocks)),
+        check(self._L.smol_csum_tool_set_max_blocks(self._h, int(max_blocks)),
               "smol_csum_tool_set_max_blocks")
 
 

@@ -57,6 +57,28 @@ def inline_ipv6_packets(rel: str):
     return out
 
 
+def hop_by_hop_packets(rel: str):
+    """The IPv6 packets with a Hop-by-Hop header of the ``hop_by_hop_*`` iface tests, with the
+    response each test asserts for ``process_ipv6``: ``None`` (dropped silently), an ICMPv6
+    ParamProblem (dropped, with an error reply) or an EchoReply (accepted: the ICMPv6 echo request
+    behind the header passed its checksum gate)."""
+    text = _read(rel)
+    out = []
+    for m in re.finditer(r"fn (hop_by_hop_\w+)\(", text):
+        body_end = text.find("\n}\n", m.end())
+        body = text[m.end(): body_end]
+        d = re.search(r"let data = \[(.*?)\];", body, re.S)
+        r = re.search(r"let response = (None|Some\(.*?IpPayload::Icmpv6\(Icmpv6Repr::(\w+))", body, re.S)
+        if not d or not r:
+            raise SystemExit(f"{rel}: {m.group(1)} has no data / response")
+        resp = "None" if r.group(1) == "None" else r.group(2)
+        line = text[: m.end() + d.start()].count("\n") + 1
+        out.append({"name": m.group(1), "kind": "ip", "bytes": _parse_array(d.group(1)).hex(),
+                    "response": resp, "dropped": resp != "EchoReply",
+                    "cite": f"{rel}:{line} ({m.group(1)}: process_ipv6 returns {resp})"})
+    return out
+
+
 V4_A = "c0a80101"  # 192.168.1.1 (udp.rs:373, tcp.rs:1240)
 V4_B = "c0a80102"  # 192.168.1.2
 FE80_1 = "fe800000000000000000000000000001"  # icmpv6.rs:851, ndisc.rs:466
@@ -228,6 +250,8 @@ def main():
         packets.append({"kind": "ip", "bytes": b.hex(), "cite": f"src/iface/interface/tests/ipv6.rs:{line}",
                         "expect": "icmpv6 verified by Icmpv6Repr::parse(default caps) in parse_ipv6"})
 
+    hbh = hop_by_hop_packets("src/iface/interface/tests/ipv6.rs")
+
     corpus_dir = os.path.join(REF, "fuzz/corpus/packet_parser")
     corpus = []
     for fn in sorted(os.listdir(corpus_dir)):
@@ -244,6 +268,7 @@ def main():
         "reference": "smoltcp 0.13.1 (/root/reference, Cargo.toml:3)",
         "kat": kats,
         "iface_ipv6_packets": packets,
+        "iface_ipv6_hop_by_hop": hbh,
         "fuzz_corpus_frames": corpus,
         "sixlowpan_nhc_udp": nhc,
         "pretty_print": pretty,
@@ -252,7 +277,7 @@ def main():
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)
     print(f"wrote {OUT}: {len(kats)} KATs, {len(packets)} iface IPv6 packets, {len(corpus)} frames, "
-          f"{len(nhc)} 6LoWPAN NHC UDP packets")
+          f"{len(nhc)} 6LoWPAN NHC UDP packets, {len(hbh)} Hop-by-Hop packets")
 
 
 if __name__ == "__main__":

@@ -39,6 +39,40 @@ def hbh(next_header: int, length_units: int, rng) -> bytes:
     return bytes([next_header, length_units]) + bytes(body)
 
 
+def hbh_opts(next_header: int, opts: bytes, pad: bool = True) -> bytes:
+    """IPv6 Hop-by-Hop header carrying the option bytes `opts` as given (valid or not), padded with
+    Pad1 options (zero bytes) to a multiple of 8 bytes (pad=False: `opts` must already fit)."""
+    n = len(opts) + 2
+    total = (n + 7) // 8 * 8
+    body = bytes(opts) + bytes(total - n if pad else 0)
+    assert (len(body) + 2) % 8 == 0
+    return bytes([next_header, (len(body) + 2) // 8 - 1]) + body
+
+
+def random_hbh_options(rng, max_opts: int = 7) -> bytes:
+    """Random option TLVs for process_hopbyhop (src/iface/interface/ipv6.rs:282-313): Pad1, PadN,
+    RouterAlert (right and wrong data length), unknown types of every failure action, Rpl (0x63),
+    and now and then a truncated last option."""
+    out = bytearray()
+    unknown = [0x0F, 0x1E, 0x3F, 0x40, 0x7F, 0x80, 0xC2, 0x63, 0x3E]  # skip (00) and discard (01/10/11)
+    for _ in range(int(rng.integers(0, max_opts + 1))):
+        c = int(rng.integers(0, 6))
+        if c == 0:
+            out += b"\x00"  # Pad1
+        elif c == 1:
+            dl = int(rng.integers(0, 6))
+            out += bytes([1, dl]) + bytes(dl)  # PadN
+        elif c == 2:
+            dl = 2 if rng.random() < 0.8 else int(rng.integers(0, 5))
+            out += bytes([5, dl]) + rand_bytes(rng, dl)  # RouterAlert
+        else:
+            dl = int(rng.integers(0, 6))
+            out += bytes([unknown[int(rng.integers(0, len(unknown)))], dl]) + rand_bytes(rng, dl)
+    if rng.random() < 0.15 and out:
+        out = out[:-int(rng.integers(1, min(3, len(out)) + 1))]  # a truncated last option
+    return bytes(out)
+
+
 def udp(sport: int, dport: int, payload: bytes, csum: int = 0, length: int | None = None) -> bytes:
     ln = 8 + len(payload) if length is None else length
     return be16(sport) + be16(dport) + be16(ln) + be16(csum) + payload

@@ -135,3 +135,17 @@ def test_phy_policy_mirror():
     assert not Checksum.None_.rx() and not Checksum.None_.tx()
     assert ChecksumCapabilities().as_tuple() == (0, 0, 0, 0, 0)
     assert ChecksumCapabilities.ignored().as_tuple() == (3, 3, 3, 3, 3)
+
+
+def test_variant_lists():
+    """The product library runs the defaults and one fallback per operation; the experiments build
+    (when it has been built) every measured variant besides (csum_api.cpp variant_built)."""
+    from smoltcp_amd import _lib
+
+    L = _lib.lib()
+    built = [v for v in range(-1, 128) if L.smol_csum_tool_variant_built(v)]
+    assert built == [-1, 5, 7, 13, 17, 21, 39], built
+    if os.path.exists(_lib.EXP_LIB_PATH):
+        X = _lib.lib(_lib.EXP_LIB_PATH)
+        exp = {v for v in range(-1, 128) if X.smol_csum_tool_variant_built(v)}
+        assert set(built) < exp and {0, 1, 3, 4, 16, 19, 23, 28, 29, 31, 37, 38, 64 + 37} <= exp

@@ -20,6 +20,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from smoltcp_amd import engine as E  # noqa: E402
+from tests.engines import VariantEngine  # noqa: E402
 
 V4A, V4B = bytes([10, 1, 2, 3]), bytes([10, 4, 5, 6])
 V6A = bytes(range(0x20, 0x30))
@@ -29,7 +30,7 @@ V6B = bytes(range(0x40, 0x50))
 @pytest.fixture(scope="module")
 def eng():
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
-    e = E.ChecksumEngine(0)
+    e = VariantEngine(0)
     yield e
     e.close()
 
@@ -183,6 +184,8 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
         # lane-shuffle variants (11, 16)
         for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (8, 0), (8, 7), (16, 0), (16, 7), (17, 0),
                                (17, 7), (21, 0), (21, 7)):
+            if not eng.has(variant):
+                continue
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,
                  base=base, seed=n + variant)
 
@@ -193,6 +196,7 @@ COPY_VARIANTS = [-1, 1, 8, 11, 16, 17, 21]
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 @pytest.mark.parametrize("shape", [-1, 0, 1, 2, 3, 4, 5, 7])
 def test_copy_emit_mixed_packed(eng, shape, variant):
+    eng.need(variant)
     rng = np.random.default_rng(10 + shape)
     recs, spec = [], []
     for i in range(1200):
@@ -205,6 +209,7 @@ def test_copy_emit_mixed_packed(eng, shape, variant):
 
 @pytest.mark.parametrize("variant", [-1, 16, 17, 21])
 def test_copy_emit_packed_zero_gaps(eng, variant):
+    eng.need(variant)
     """C3-style batch: TCP records of U[64, 9000] bytes packed back to back with no gap (odd
     offsets), so neighbouring records share cache lines.  Copy-emit rewrites every byte of a record
     (include/smolcsum.h, INTEGRATION.md §4.1.1); a neighbour's bytes must survive bit for bit."""
@@ -223,6 +228,7 @@ def test_copy_emit_packed_zero_gaps(eng, variant):
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 def test_copy_emit_all_alignments(eng, variant):
+    eng.need(variant)
     """dst offsets and source offsets cover every residue mod 16."""
     rng = np.random.default_rng(7)
     recs, spec = [], []
@@ -238,6 +244,7 @@ def test_copy_emit_all_alignments(eng, variant):
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 def test_copy_over_fields_and_edge_ranges(eng, variant):
+    eng.need(variant)
     rng = np.random.default_rng(21)
     recs, spec = [], []
     for i in range(400):
@@ -278,7 +285,7 @@ def test_copy_emit_caps_and_rejected_records(eng):
         recs.append(r)
         spec.append((hdr, len(r) - hdr))
     for caps in [(3, 3, 3, 3, 3), (1, 2, 1, 2, 1), (0, 0, 0, 0, 0)]:
-        for variant in (-1, 8, 11, 16, 17):
+        for variant in eng.avail((-1, 8, 11, 16, 17)):
             _run(eng, recs, spec, caps=caps, gap_seed=8, seed=12, variant=variant)
 
 
@@ -293,6 +300,7 @@ def test_copy_emit_errors(eng):
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 def test_copy_emit_far_fields(eng, variant):
+    eng.need(variant)
     """IPv6 records whose Hop-by-Hop header pushes the TCP / UDP checksum field past the 128-B
     header window (or across its edge): the field must still be the emitted value, whether the copy
     range covers it or not, at every record alignment."""
@@ -327,6 +335,7 @@ def test_copy_emit_far_fields(eng, variant):
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 def test_copy_emit_tiny_records(eng, variant):
+    eng.need(variant)
     """Records of 0 .. 47 bytes (shorter than the header window, than one 16-B chunk, or empty)
     packed at odd offsets, with copy ranges anywhere inside them (or not fitting)."""
     rng = np.random.default_rng(33)
@@ -347,6 +356,7 @@ def test_copy_emit_tiny_records(eng, variant):
 
 @pytest.mark.parametrize("variant", [-1, 16, 17, 21])
 def test_copy_emit_packed_fields_in_last_line(eng, variant):
+    eng.need(variant)
     """Records packed back to back (no gaps) where some hold their L4 checksum field in their last
     128-B line (an IPv6 Hop-by-Hop header of 256-2000 B before a short TCP / UDP segment), between
     ordinary ones: the fields and the neighbours' bytes, which share those lines, must come out

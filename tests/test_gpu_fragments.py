@@ -21,12 +21,13 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from smoltcp_amd import engine as E  # noqa: E402
+from tests.engines import VariantEngine  # noqa: E402
 
 
 @pytest.fixture(scope="module")
 def eng():
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
-    e = E.ChecksumEngine(0)
+    e = VariantEngine(0)
     yield e
     e.close()
 

@@ -21,6 +21,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from smoltcp_amd import engine as E  # noqa: E402
+from tests.engines import VariantEngine  # noqa: E402
 
 V4A, V4B = bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2])
 A6, B6 = bytes(range(16)), bytes(range(16, 32))
@@ -30,7 +31,7 @@ CAPS = [(0, 0, 0, 0, 0), (3, 0, 0, 0, 0), (2, 0, 0, 3, 0), (0, 0, 0, 1, 0), (1, 
 @pytest.fixture(scope="module")
 def eng():
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
-    e = E.ChecksumEngine(0)
+    e = VariantEngine(0)
     yield e
     e.close()
 
@@ -98,11 +99,11 @@ def _corpus_frame(golden):
 def test_icmpv4_unreachable_corpus_frame_every_path(eng, golden):
     """The zeroed corpus frame comes back byte for byte from every emit path."""
     orig, z, _ = _corpus_frame(golden)
-    for variant in (-1, 7, 3, 4, 1, 5, 0, 6):  # tile (default for descriptors) and walk
+    for variant in eng.avail((-1, 7, 3, 4, 1, 5, 0, 6)):  # tile (default for descriptors) and walk
         got, offs, lens = _emit_desc(eng, [z] * 5, E.KIND_ETH, (0, 0, 0, 0, 0), variant)
         for o, ln in zip(offs, lens):
             assert got[int(o):int(o) + int(ln)].tobytes() == orig, variant
-    for variant in (-1, 9, 10, 6, 1, 0):  # fixed stride: walk kernel (line grid default)
+    for variant in eng.avail((-1, 9, 10, 6, 1, 0)):  # fixed stride: walk kernel (line grid default)
         for stride, off in ((len(z), 0), (601, 3), (640, 0)):
             got = _emit_fixed(eng, z, 37, stride, E.KIND_ETH, (0, 0, 0, 0, 0), variant, off)
             for i in range(37):
@@ -155,7 +156,7 @@ def test_icmpv4_errors_random_vs_oracle(eng):
     ip = _icmp4_errors(rng, 500)
     eth = [P.eth(r) for r in _icmp4_errors(rng, 200)]
     for caps in CAPS:
-        for variant in (-1, 3, 1, 5):
+        for variant in eng.avail((-1, 3, 1, 5)):
             _emit_desc(eng, ip, E.KIND_IP, caps, variant)
             _emit_desc(eng, eth, E.KIND_ETH, caps, variant)
 
@@ -168,7 +169,7 @@ def test_icmpv4_error_fixed_stride_vs_oracle(eng):
     inner = P.ipv4(bytes([127, 0, 0, 2]), bytes([127, 0, 0, 1]), 17, udp)
     pkt = P.ipv4(bytes([127, 0, 0, 1]), bytes([127, 0, 0, 2]), 1, P.icmp4_error(3, 3, inner))
     for caps in CAPS:
-        for variant in (-1, 9, 1):
+        for variant in eng.avail((-1, 9, 1)):
             for stride, off in ((len(pkt), 0), (len(pkt) + 1, 1), (256, 7)):
                 _emit_fixed(eng, pkt, 301, stride, E.KIND_IP, caps, variant, off)
 
@@ -191,7 +192,7 @@ def test_icmpv6_check_len_every_type(eng, golden):
     P.oracle_emit_records(buf, offs, lens, E.KIND_IP)
     filled = [buf[int(o):int(o) + int(ln)].tobytes() for o, ln in zip(offs, lens)]
     assert host.size == sum(len(r) for r in recs)
-    for variant in (-1, 3, 4, 7, 1, 0):
+    for variant in eng.avail((-1, 3, 4, 7, 1, 0)):
         for rs, kind in ((filled, E.KIND_IP), ([P.eth(r, 0x86DD) for r in filled], E.KIND_ETH)):
             b2, o2, l2 = P.pack(rs, gap_rng=np.random.default_rng(variant + 5))
             batch = E.Batch.from_records(o2, l2, kind, "cuda:0")

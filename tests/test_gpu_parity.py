@@ -22,6 +22,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from smoltcp_amd import engine as E  # noqa: E402
+from tests.engines import VariantEngine  # noqa: E402
 
 CAPS_DEFAULT = (0, 0, 0, 0, 0)
 V4A, V4B = bytes([192, 168, 1, 1]), bytes([192, 168, 1, 2])
@@ -31,7 +32,7 @@ SHAPES = [0, 1, 2, 3, 4, 5, 6, 7, 8]
 @pytest.fixture(scope="module")
 def eng():
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
-    e = E.ChecksumEngine(0)
+    e = VariantEngine(0)
     yield e
     e.close()
 
@@ -210,7 +211,7 @@ def test_packed_mixed_lengths_descriptors(eng):
     ref_v = oracle.batch_verify(host, desc, n)
     ref = host.copy()
     oracle.batch_emit(ref, desc, n)
-    for variant in (-1, 5, 13, 1, 7, 23, 24, 25, 26, 27, 28, 29):
+    for variant in eng.avail((-1, 5, 13, 1, 7, 23, 24, 25, 26, 27, 28, 29)):
         for shape in SHAPES:
             eng.set_shape(shape)
             eng.set_variant(variant)
@@ -364,6 +365,55 @@ def test_ipv6_hop_by_hop(eng):
     _run_records(eng, [P.eth(r, 0x86DD) for r in recs], E.KIND_ETH, gap_seed=15)
 
 
+def test_iface_ipv6_hop_by_hop_packets(eng, golden):
+    """The reference's hop_by_hop_* packets (src/iface/interface/tests/ipv6.rs:151,200,232,290):
+    skip -> accepted, the three discards -> MALFORMED (process_hopbyhop drops them before the L4
+    gate, ipv6.rs:282-313); random gaps, every shape."""
+    hbh = golden["iface_ipv6_hop_by_hop"]
+    recs = [bytes.fromhex(p["bytes"]) for p in hbh] * 8
+    for shape in (-1, 0, 1, 3, 5, 7, 8):
+        st, _, _, _ = _run_records(eng, recs, E.KIND_IP, gap_seed=3 + shape, shape=shape)
+        for p, s in zip(hbh * 8, st):
+            if p["dropped"]:
+                assert s & E.ST_MALFORMED and not s & E.ST_ACCEPT, (p["cite"], shape, hex(s))
+            else:
+                assert s & E.ST_ACCEPT and s & E.ST_L4_VALID, (p["cite"], shape, hex(s))
+
+
+def test_ipv6_hop_by_hop_options(eng):
+    """Random Hop-by-Hop options (Pad1, PadN, RouterAlert of right and wrong length, unknown types of
+    every failure action, Rpl, truncated TLVs, more than 4 options) against the oracle, on IP and
+    Ethernet records, fixed-stride and descriptor batches; options behind long PadN fillers put the
+    tested options past the LDS window."""
+    rng = np.random.default_rng(21)
+    recs = []
+    for i in range(400):
+        opts = P.random_hbh_options(rng)
+        if i % 5 == 4:  # two long PadN options first: the tested options sit past the window
+            opts = bytes([1, 250]) + bytes(250) + bytes([1, 120]) + bytes(120) + opts
+        nh = [6, 17, 58][i % 3]
+        pl = P.rand_bytes(rng, int(rng.integers(0, 120)))
+        l4 = {6: P.tcp(3, 4, pl), 17: P.udp(3, 4, pl), 58: P.icmp_echo(128, pl)}[nh]
+        recs.append(P.ipv6(P.rand_bytes(rng, 16), P.rand_bytes(rng, 16), 0, P.hbh_opts(nh, opts) + l4))
+    # emit first (valid checksums), so that verify's status says whether the options dropped it
+    buf, offs, lens = P.pack(recs)
+    P.oracle_emit_records(buf, offs, lens, np.full(len(recs), E.KIND_IP, np.uint8), CAPS_DEFAULT)
+    recs = [buf[int(o):int(o) + int(n)].tobytes() for o, n in zip(offs, lens)]
+    st, _, _, _ = _run_records(eng, recs, E.KIND_IP, gap_seed=22)
+    dropped = sum(bool(s & E.ST_MALFORMED) for s in st)
+    assert 0.2 * len(recs) < dropped < 0.9 * len(recs), dropped
+    _run_records(eng, [P.eth(r, 0x86DD) for r in recs], E.KIND_ETH, gap_seed=23, shape=1)
+    # fixed stride: the records padded to one length
+    L = max(len(r) for r in recs)
+    fixed = [r + bytes(L - len(r)) for r in recs]
+    host = np.frombuffer(b"".join(fixed) + bytes(16), dtype=np.uint8).copy()
+    d = _dev(host)
+    batch = E.Batch.fixed(len(fixed), L, L, E.KIND_IP)
+    st = eng.verify(d, batch).cpu().numpy()
+    ref = oracle.batch_verify(host, None, len(fixed), L, L, E.KIND_IP, CAPS_DEFAULT)
+    assert np.array_equal(st, ref)
+
+
 def test_malformed_and_garbage(eng):
     """Length-field lies, truncation, wrong versions, random bytes: statuses match, and emit
     writes exactly where the oracle writes."""
@@ -505,7 +555,12 @@ def test_emit_variants_match_oracle(eng, profile, kind):
                     (23, -1, 0, (0, 0, 0, 0, 0)), (23, 7, 3, (3, 2, 2, 3, 3)), (23, 0, 5, (2, 3, 0, 1, 0)),
                     (24, -1, 0, (0, 0, 0, 0, 0)), (25, 7, 0, (0, 0, 0, 0, 0)), (26, -1, 0, (0, 0, 0, 0, 0)),
                     (26, 1, 3, (2, 3, 0, 1, 0)), (27, 8, 0, (0, 0, 0, 0, 0)), (28, 8, 5, (0, 0, 0, 0, 0)),
-                    (29, -1, 0, (0, 0, 0, 0, 0)), (29, 7, 3, (3, 2, 2, 3, 3))]:
+                    (29, -1, 0, (0, 0, 0, 0, 0)), (29, 7, 3, (3, 2, 2, 3, 3)),
+                    (37, -1, 0, (0, 0, 0, 0, 0)), (37, 7, 3, (3, 2, 2, 3, 3)), (37, 0, 0, (2, 3, 0, 1, 0)),
+                    (38, -1, 0, (0, 0, 0, 0, 0)), (38, 0, 5, (0, 0, 0, 0, 0)),
+                    (39, -1, 0, (0, 0, 0, 0, 0)), (39, 7, 3, (3, 2, 2, 3, 3)), (39, 0, 5, (2, 3, 0, 1, 0))]:
+                if not eng.has(variant):
+                    continue
                 _emit_case(eng, host, off, n, stride, L, kind, caps, variant, shape, blocks)
 
 
@@ -533,11 +588,11 @@ def test_emit_neighbour_fields(eng):
         for off in (0, 5, 40, 63):
             host = np.concatenate([rng.integers(0, 256, off, dtype=np.uint8),
                                    np.frombuffer(b"".join(recs), np.uint8), np.zeros(128, np.uint8)])
-            for variant in (-1, 5, 6, 1, 0, 9, 19, 23, 24, 25, 26, 27, 28, 29):
+            for variant in eng.avail((-1, 5, 6, 1, 0, 9, 19, 23, 24, 25, 26, 27, 28, 29)):
                 _emit_case(eng, host, off, n, stride, stride, E.KIND_IP, CAPS_DEFAULT, variant)
             # whole field segments with several records per group (neighbours out of step)
             for blocks in (1, 3, 5):
-                for variant in (19, 23, 26, 28, 29):
+                for variant in eng.avail((19, 23, 26, 28, 29, 39)):
                     _emit_case(eng, host, off, n, stride, stride, E.KIND_IP, CAPS_DEFAULT, variant, -1, blocks)
 
 
@@ -564,7 +619,7 @@ def _expected_launch(variant, op, has_desc):
     if variant in (3, 4, 7):
         return ("csum_tile_kernel", {3: 0, 4: 1, 7: 2}[variant])
     emit_fixed = op == "emit" and not has_desc
-    if variant in (9, 10, 29):
+    if variant in (9, 10, 29, 37, 38, 39):
         return ("csum_kernel", variant if emit_fixed else 5)
     if 23 <= variant <= 28:
         if op == "emit":
@@ -573,8 +628,9 @@ def _expected_launch(variant, op, has_desc):
     return ("csum_kernel", variant)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 13, 19, 23, 24, 25, 26, 27, 28, 29])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 13, 19, 23, 24, 25, 26, 27, 28, 29, 37, 38, 39])
 def test_variants_fixed_stride(eng, variant):
+    eng.need(variant)
     """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
     the oracle on fixed-stride batches: strides equal to the record length (neighbours share
     lines), odd strides, gaps, every shape, natural and persistent grids."""

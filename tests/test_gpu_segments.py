@@ -26,6 +26,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from smoltcp_amd import engine as E  # noqa: E402
+from tests.engines import VariantEngine  # noqa: E402
 
 SEG_VARIANTS = (23, 24, 25, 26, 27, 28)
 SHAPES = [0, 1, 2, 3, 4, 5, 6, 7, 8]
@@ -36,7 +37,7 @@ A6, B6 = bytes(range(16)), bytes(range(16, 32))
 @pytest.fixture(scope="module")
 def eng():
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
-    e = E.ChecksumEngine(0)
+    e = VariantEngine(0)
     yield e
     e.close()
 
@@ -70,7 +71,7 @@ def _desc_case(eng, host, offs, lens, kinds, flags=0, variants=SEG_VARIANTS, blo
     desc = P.oracle_desc(offs, lens, kinds, flags)
     ref = host.copy()
     ref_st = oracle.batch_emit(ref, desc, n)
-    for variant in variants:
+    for variant in eng.avail(variants):
         for shape in shapes:
             for blocks in blocks_list:
                 d = torch.from_numpy(host.copy()).cuda()
@@ -230,7 +231,9 @@ def test_emit_write_set_concurrent(eng, gap):
     s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
     K = 120
     for variant, batch in ((19, fixed), (29, fixed), (-1, fixed), (23, fixed), (26, desc_batch), (28, desc_batch),
-                           (-1, desc_batch)):
+                           (-1, desc_batch), (37, fixed), (39, fixed)):
+        if not eng.has(variant):
+            continue
         d = torch.from_numpy(host0.copy()).cuda()
         torch.cuda.synchronize()
         eng.set_variant(variant)
@@ -263,7 +266,7 @@ def test_field_stores_flag(eng):
     ref = host.copy()
     oracle.batch_emit(ref, desc, n)
     batch = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0", batch_flags=E.BATCH_FIELD_STORES)
-    for variant in (-1, 19, 23, 26, 27, 28, 29, 7):
+    for variant in eng.avail((-1, 19, 23, 26, 27, 28, 29, 39, 7)):
         d = torch.from_numpy(host.copy()).cuda()
         eng.set_variant(variant)
         try:

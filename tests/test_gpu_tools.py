@@ -6,13 +6,14 @@ import pytest
 import torch
 
 from smoltcp_amd import engine as E
+from tests.engines import VariantEngine
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
 def eng():
-    e = E.ChecksumEngine(0)
+    e = VariantEngine(0)
     yield e
     e.close()
 
@@ -47,7 +48,7 @@ def test_last_launch_families(eng):
     eng.synth(buf, b, E.SYNTH_UDP4, seed=1)
     eng.emit(buf, b)
     ll = eng.last_launch()
-    assert (ll["kernel"], ll["variant"], ll["G"]) == ("csum_kernel", 29, 8), ll
+    assert (ll["kernel"], ll["variant"], ll["G"]) == ("csum_kernel", 39, 8), ll
     eng.verify(buf, b)
     ll = eng.last_launch()
     assert (ll["kernel"], ll["variant"]) == ("csum_kernel", 5), ll

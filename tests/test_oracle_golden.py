@@ -167,6 +167,54 @@ def test_iface_ipv6_packets(golden):
         assert pyref.icmpv6_verify(b[40:40 + plen], b[8:24], b[24:40]), p["cite"]
 
 
+def test_iface_ipv6_hop_by_hop_packets(golden):
+    """The four hop_by_hop_* packets of src/iface/interface/tests/ipv6.rs:151,200,232,290: the skip
+    option's packet is accepted (its ICMPv6 echo request passes the checksum gate), the three whose
+    options make process_hopbyhop drop the packet (ipv6.rs:282-313) are MALFORMED: dropped before any
+    checksum is looked at.  Emit does not parse the options: it fills all four the same way."""
+    L = oracle.lib()
+    caps = oracle.caps_c()
+    hbh = golden["iface_ipv6_hop_by_hop"]
+    assert [p["dropped"] for p in hbh] == [False, True, True, True]
+    for p in hbh:
+        b = bytes.fromhex(p["bytes"])
+        a = _arr(b)
+        st = L.oracle_record_verify(a.ctypes.data, a.size, 1, ctypes.byref(caps))
+        if p["dropped"]:
+            assert st & ST_MALFORMED and not st & ST_ACCEPT, (p["cite"], hex(st))
+        else:
+            assert st & ST_ACCEPT and st & ST_L4_VALID and not st & ST_MALFORMED, (p["cite"], hex(st))
+        hlen = (b[41] + 1) * 8
+        assert pyref.hbh_options_drop(b[42:40 + hlen]) == p["dropped"], p["cite"]
+        # emit: the ICMPv6 checksum behind the header is filled (the multicast packet reuses the
+        # others' ICMPv6 bytes under another destination, so only a correct checksum is asserted)
+        e = _arr(b)
+        e[40 + hlen + 2:40 + hlen + 4] = 0
+        L.oracle_record_emit(e.ctypes.data, e.size, 1, ctypes.byref(caps))
+        plen = b[4] << 8 | b[5]
+        assert pyref.icmpv6_verify(e.tobytes()[40 + hlen:40 + plen], b[8:24], b[24:40]), p["cite"]
+        if b[24] != 0xFF:
+            assert e.tobytes() == b, p["cite"]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_hbh_options_c_matches_pyref(seed):
+    """The C restatement of process_hopbyhop's option walk against pyref's literal one (iterator +
+    4-entry Vec), on random option bytes biased towards Pad1 / PadN / RouterAlert / discard types."""
+    L = oracle.lib()
+    rng = np.random.default_rng(seed)
+    types = np.array([0, 1, 5, 2, 0x0F, 0x40, 0x80, 0xC0, 0x63], dtype=np.uint8)
+    for _ in range(20000):
+        n = int(rng.integers(0, 40))
+        a = rng.integers(0, 256, n).astype(np.uint8)
+        m = rng.random(n) < 0.6
+        a[m] = rng.choice(types, int(m.sum()))
+        s = rng.random(n) < 0.5
+        a[s] = rng.integers(0, 4, int(s.sum()))
+        got = L.oracle_hbh_options_drop(a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), n)
+        assert bool(got) == pyref.hbh_options_drop(a.tobytes()), a.tobytes().hex()
+
+
 CORPUS_EXPECT = {
     # frame: (IP header valid, L4 fully valid, L4 partial (TX-offload) checksum, unsupported)
     "arp.bin": None,

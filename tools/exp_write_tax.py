@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Experiment (round 5): what one scattered field write costs HBM, against the spacing of the written
+lines and the order they are written in.
+
+For each spacing S (256 B .. 8 KB) the same 2^21 writes (2-B fields at byte 10 of each S-byte slot,
+or the whole 64-B segment holding that byte) go into a buffer of 2^21 * S bytes, in address order,
+shuffled within windows of 8192 writes (about what the tile kernel's resident workgroups have in
+flight), or fully shuffled.  Each write pass is timed two ways, interleaved on one box:
+  alone     the write pass by itself, after a read stream over another buffer has evicted the
+            caches (the dirty lines then leave L2 / the Infinity Cache during the next flush);
+  in_read   the write pass followed by a read-only stream over a 4.7-GB buffer, minus that stream
+            alone: what the writes cost when their write-back lands inside a read stream (emit).
+Usage: [SPACINGS=256,512,...] [N=2097152] [ROUNDS=3] exp_write_tax.py"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from smoltcp_amd import engine as E  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    eng = E.ChecksumEngine(0)
+    N = int(os.environ.get("N", str(1 << 21)))
+    spacings = [int(x) for x in os.environ.get("SPACINGS", "256,512,1024,1536,2048,4608,8192").split(",")]
+    rounds = int(os.environ.get("ROUNDS", "3"))
+    buf = torch.zeros(N * max(spacings) + 64, dtype=torch.uint8, device=dev)
+    rd = torch.zeros(4_700_000_000 // 16 * 16, dtype=torch.uint8, device=dev)  # the read stream (C3's size)
+    flush = torch.zeros(1 << 30, dtype=torch.uint8, device=dev)
+    sink = torch.zeros(1, dtype=torch.int32, device=dev)
+    vals = torch.full((N,), 0x1234, dtype=torch.int16, device=dev)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    W = 8192
+
+    def orders(S):
+        a = torch.arange(N, dtype=torch.int64) * S + 10
+        win = a.view(-1, W)
+        perm = torch.argsort(torch.rand(win.shape, generator=g), dim=1)
+        yield "address", a.to(dev)
+        yield "window8k", torch.gather(win, 1, perm).reshape(-1).to(dev)
+        yield "random", a[torch.randperm(N, generator=g)].to(dev)
+
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    def t_alone(addrs, flags, reps=5):
+        out = []
+        for _ in range(reps):
+            eng.stream_read(flush, sink)
+            eng.stream_read(flush, sink)
+            a, b = ev(), ev()
+            a.record()
+            eng.field_scatter(buf, addrs, vals, nt=flags)
+            b.record()
+            torch.cuda.synchronize()
+            out.append(a.elapsed_time(b))
+        return sorted(out)[len(out) // 2]
+
+    def t_read(addrs, flags, reps=8):
+        def once(with_writes):
+            if with_writes:
+                eng.field_scatter(buf, addrs, vals, nt=flags)
+            eng.stream_read(rd, sink)
+        for w in (False, True):
+            once(w)
+        res = {}
+        for w in (False, True, False, True):
+            a, b = ev(), ev()
+            a.record()
+            for _ in range(reps):
+                once(w)
+            b.record()
+            torch.cuda.synchronize()
+            res.setdefault(w, []).append(a.elapsed_time(b) / reps)
+        return min(res[False]), min(res[True])
+
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:
+        eng.stream_read(rd, sink)
+        torch.cuda.synchronize()
+    for rnd in range(rounds):
+        for S in spacings:
+            for oname, addrs in orders(S):
+                for form, flags in (("field2", 0), ("seg64", 2)):
+                    alone = t_alone(addrs, flags)
+                    r0, r1 = t_read(addrs, flags)
+                    print(json.dumps({"round": rnd, "spacing": S, "order": oname, "form": form, "writes": N,
+                                      "alone_ms": round(alone, 4), "read_ms": round(r0, 4),
+                                      "read_plus_writes_ms": round(r1, 4), "in_read_ms": round(r1 - r0, 4),
+                                      "ns_per_write_in_read": round((r1 - r0) * 1e6 / N, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
