@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SMOLCSUM_ABI_VERSION 5
+#define SMOLCSUM_ABI_VERSION 6
 
 /* ---- error codes ------------------------------------------------------------------------ */
 enum {
@@ -152,8 +152,12 @@ enum {
                                   looked at: a check_len() on the path failed, or (verify only) a
                                   port Repr::parse rejects first — UDP destination port 0
                                   (udp.rs:246-248), TCP source or destination port 0
-                                  (tcp.rs:910-915).  The L4 bits are then not evaluated (set).
-                                  Emit never rejects ports: Repr::emit does not check them.      */
+                                  (tcp.rs:910-915) — or (verify only, ABI 6) the iface drops an
+                                  IPv6 packet on its Hop-by-Hop options: an option that fails to
+                                  parse, or an unknown option whose type asks for a discard
+                                  (process_hopbyhop, iface/interface/ipv6.rs:282-313).  The L4 bits
+                                  are then not evaluated (set).  Emit never rejects ports or
+                                  options: Repr::emit does not check them.                       */
     SMOL_ST_UNSUPPORTED = 0x40,/* no L4 checksum on this record's path: IPv4 fragment, protocol
                                   smoltcp does not checksum, IPv6 next header other than a
                                   leading Hop-by-Hop + TCP/UDP/ICMPv6, non-IP ethertype          */
@@ -326,7 +330,10 @@ int smol_csum_batch_nhc_udp_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smo
                                  uint8_t* d_status, void* stream);
 
 /* UdpNhcRepr::parse's checksum gate (src/wire/sixlowpan/nhc.rs:693-729): SMOL_ST_MALFORMED when
- * UdpNhcPacket::check_len (nhc.rs:486-500) or the dispatch test fails; otherwise under
+ * UdpNhcPacket::check_len (nhc.rs:486-500) or the dispatch test fails, or (ABI 5) when an inline
+ * destination port (ports modes 0b00 / 0b10) is 0: the iface parses the decompressed header with
+ * UdpRepr::parse, which drops it (src/iface/interface/sixlowpan.rs:745-775, udp.rs:246-248);
+ * otherwise under
  * caps.udp.rx() an inline checksum must equal the one computed over the ports as the packet
  * accessors read them (nhc.rs:513-577); an elided checksum (C bit set) is not checked.  The IP
  * bits are always set (no IPv4 header). */

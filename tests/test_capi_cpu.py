@@ -31,7 +31,7 @@ def test_library_loads_and_exports_all_declared_symbols():
         assert hasattr(L, name), f"{name} declared in include/ but not exported"
     assert sorted(_lib.ABI_SYMBOLS) == _declared("smolcsum.h")
     assert sorted(_lib.TOOL_SYMBOLS) == _declared("smolcsum_tools.h")
-    assert L.smol_csum_abi_version() == 5
+    assert L.smol_csum_abi_version() == 6
 
 
 def test_library_is_a_gfx950_code_object():

@@ -735,6 +735,32 @@ def test_xcd_remap(eng, xcd):
         eng.set_xcd_remap(-1)
 
 
+@pytest.mark.parametrize("xcd", [1, 256])
+def test_xcd_remap_large_grid(eng, xcd):
+    """The XCD orders over a grid large enough that xcd_chunk permutes blocks at the library's
+    default grain for big verify batches (K = 256: the first 8 * 256 = 2048 workgroups): 2^16 + 5
+    fixed-stride records of 1500 B (98 MB; 8 x 7 emit / verify: 2049 workgroups), corrupted 1 in 7,
+    against the oracle over the whole buffer."""
+    n, L = (1 << 16) + 5, 1500
+    buf = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+    batch = E.Batch.fixed(n, L, L, E.KIND_IP)
+    eng.synth(buf, batch, E.SYNTH_UDP4, seed=xcd + 77)
+    eng.corrupt(buf, batch, every=7, seed=xcd)
+    host = buf.cpu().numpy().copy()
+    assert (n + 31) // 32 >= 8 * 256  # workgroups of 32 records (G = 8)
+    ref_v = oracle.batch_verify(host.copy(), None, n, L, L, E.KIND_IP, CAPS_DEFAULT)
+    ref_e = host.copy()
+    oracle.batch_emit(ref_e, None, n, L, L, E.KIND_IP, CAPS_DEFAULT)
+    eng.set_xcd_remap(xcd)
+    try:
+        st = eng.verify(buf, batch).cpu().numpy()
+        eng.emit(buf, batch)
+    finally:
+        eng.set_xcd_remap(-1)
+    assert np.array_equal(st, ref_v), xcd
+    assert np.array_equal(buf.cpu().numpy(), ref_e), xcd
+
+
 def test_launch_records(eng):
     """Batches split into consecutive launches (smol_csum_tool_set_launch_records): emit, verify
     and data over fixed-stride and descriptor batches, status arrays, copy-emit and 6LoWPAN NHC UDP,

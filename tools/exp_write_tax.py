@@ -3,13 +3,15 @@
 lines and the order they are written in.
 
 For each spacing S (256 B .. 8 KB) the same 2^21 writes (2-B fields at byte 10 of each S-byte slot,
-or the whole 64-B segment holding that byte) go into a buffer of 2^21 * S bytes, in address order,
-shuffled within windows of 8192 writes (about what the tile kernel's resident workgroups have in
-flight), or fully shuffled.  Each write pass is timed two ways, interleaved on one box:
-  alone     the write pass by itself, after a read stream over another buffer has evicted the
-            caches (the dirty lines then leave L2 / the Infinity Cache during the next flush);
-  in_read   the write pass followed by a read-only stream over a 4.7-GB buffer, minus that stream
-            alone: what the writes cost when their write-back lands inside a read stream (emit).
+or the whole 64-B segment holding that byte) go into one of R = 4 regions of 2^21 * S bytes, in
+address order, shuffled within windows of 8192 writes (about what the tile kernel's resident
+workgroups have in flight), or fully shuffled.  Passes take the regions in turn, so that a pass
+never rewrites lines the Infinity Cache still holds dirty from the previous one (as a TX path
+that fills new frames), and the steady state includes the DRAM write-back of earlier passes.
+Timed, interleaved on one box:
+  alone     K write passes back to back, per pass;
+  in_read   K (write pass + a read-only stream over a 4.7-GB buffer) minus K read streams, per pass:
+            what the writes cost when their write-back lands inside a read stream (emit).
 Usage: [SPACINGS=256,512,...] [N=2097152] [ROUNDS=3] exp_write_tax.py"""
 import json
 import os
@@ -30,55 +32,45 @@ def main():
     N = int(os.environ.get("N", str(1 << 21)))
     spacings = [int(x) for x in os.environ.get("SPACINGS", "256,512,1024,1536,2048,4608,8192").split(",")]
     rounds = int(os.environ.get("ROUNDS", "3"))
-    buf = torch.zeros(N * max(spacings) + 64, dtype=torch.uint8, device=dev)
+    R = 4
+    buf = torch.zeros(R * N * max(spacings) + 64, dtype=torch.uint8, device=dev)
     rd = torch.zeros(4_700_000_000 // 16 * 16, dtype=torch.uint8, device=dev)  # the read stream (C3's size)
-    flush = torch.zeros(1 << 30, dtype=torch.uint8, device=dev)
     sink = torch.zeros(1, dtype=torch.int32, device=dev)
     vals = torch.full((N,), 0x1234, dtype=torch.int16, device=dev)
     g = torch.Generator(device="cpu").manual_seed(5)
     W = 8192
+    K = 16
 
     def orders(S):
         a = torch.arange(N, dtype=torch.int64) * S + 10
         win = a.view(-1, W)
         perm = torch.argsort(torch.rand(win.shape, generator=g), dim=1)
-        yield "address", a.to(dev)
-        yield "window8k", torch.gather(win, 1, perm).reshape(-1).to(dev)
-        yield "random", a[torch.randperm(N, generator=g)].to(dev)
+        for name, x in (("address", a), ("window8k", torch.gather(win, 1, perm).reshape(-1)),
+                        ("random", a[torch.randperm(N, generator=g)])):
+            yield name, [(x + k * N * S).to(dev) for k in range(R)]
 
     def ev():
         return torch.cuda.Event(enable_timing=True)
 
-    def t_alone(addrs, flags, reps=5):
-        out = []
-        for _ in range(reps):
-            eng.stream_read(flush, sink)
-            eng.stream_read(flush, sink)
-            a, b = ev(), ev()
-            a.record()
-            eng.field_scatter(buf, addrs, vals, nt=flags)
-            b.record()
-            torch.cuda.synchronize()
-            out.append(a.elapsed_time(b))
-        return sorted(out)[len(out) // 2]
+    def timed(fn):
+        for k in range(R):
+            fn(k)
+        a, b = ev(), ev()
+        a.record()
+        for k in range(K):
+            fn(k % R)
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / K
 
-    def t_read(addrs, flags, reps=8):
-        def once(with_writes):
-            if with_writes:
-                eng.field_scatter(buf, addrs, vals, nt=flags)
-            eng.stream_read(rd, sink)
-        for w in (False, True):
-            once(w)
-        res = {}
-        for w in (False, True, False, True):
-            a, b = ev(), ev()
-            a.record()
-            for _ in range(reps):
-                once(w)
-            b.record()
-            torch.cuda.synchronize()
-            res.setdefault(w, []).append(a.elapsed_time(b) / reps)
-        return min(res[False]), min(res[True])
+    def t_alone(addrs, flags):
+        return timed(lambda k: eng.field_scatter(buf, addrs[k], vals, nt=flags))
+
+    def t_read(addrs, flags):
+        r0 = min(timed(lambda k: eng.stream_read(rd, sink)) for _ in range(2))
+        r1 = min(timed(lambda k: (eng.field_scatter(buf, addrs[k], vals, nt=flags), eng.stream_read(rd, sink)))
+                 for _ in range(2))
+        return r0, r1
 
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.3:
