@@ -139,7 +139,7 @@ bool variant_built(int v) {
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39);
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38);
+           (v >= 31 && v <= 38) || v == 42;
 #else
     return false;
 #endif
@@ -216,6 +216,9 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool has_desc = b->desc != nullptr;
     if (variant < 0) variant = auto_variant(mode, has_desc);
     if (mode == MODE_EMIT && (b->flags & SMOL_BATCH_FIELD_STORES)) variant = field_store_variant(variant, has_desc);
+    // the stripe kernel (variant 42) serves emit / verify of packed fixed-stride records of 1024-1520 B
+    const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
+    if (variant == 42 && !stripe) variant = walk_variant(mode, has_desc);
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
     if (tile_var && (mode == MODE_DATA || mode == MODE_COPY || d_addrs)) variant = walk_variant(mode, has_desc);
     const bool use_tile = variant == 3 || variant == 4 || variant == 7;
@@ -250,6 +253,11 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         const int cshape = ctx->shape >= 0 ? ctx->shape : ((var == 17 || var == 21) ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
+        return SMOL_OK;
+    }
+    if (stripe) {
+        hipError_t e = launch_stripe(mode, p, s);
+        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         return SMOL_OK;
     }
     if (use_tile) {

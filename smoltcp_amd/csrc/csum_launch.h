@@ -117,6 +117,10 @@ hipError_t launch_walk_nhc(int shape, int var, const KParams& p, uint32_t max_bl
 hipError_t launch_tile(int mode, int shape, int var, int tile_records, const KParams& p, uint32_t max_blocks,
                        hipStream_t s);
 
+// Stripe kernel (csum_tile.hip, variant 42): fixed-stride packed records of 1024-1520 bytes.
+bool stripe_fits(const KParams& p);
+hipError_t launch_stripe(int mode, const KParams& p, hipStream_t s);
+
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
 struct SynthParams {
     uint8_t* buf;

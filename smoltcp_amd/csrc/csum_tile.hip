@@ -118,6 +118,111 @@ __device__ __forceinline__ uint32_t region_sum(const uint32_t* row, uint64_t bas
     return acc;
 }
 
+// Phase C of one record, by one lane alone (the tile and stripe kernels): parse the header from the
+// record's LDS window row (WIN bytes from its 16-byte boundary), take the bytes outside the summed
+// span back out of `sum`, apply the gates, write the status byte or the fields of record r.
+// `sum`: the aligned-word sum of [a0 & ~15, a0 + len) (tile); EXACT: of [a0, a0 + len) (stripe).
+template <int MODE, bool EXACT>
+__device__ __forceinline__ void finish_record(const KParams& p, const uint32_t* row, uint32_t sum, uint64_t my_a0,
+                                              uint32_t my_len, uint32_t my_kind, uint64_t r) {
+    const uint32_t head = (uint32_t)(my_a0 & 15u);
+    const uint64_t base = my_a0 & ~15ull;
+    const bool odd = (my_a0 & 1u) != 0;
+    const uint32_t nch = my_len ? (uint32_t)(((my_a0 + my_len + 15) >> 4) - (my_a0 >> 4)) : 0u;
+    const uint32_t wvalid = nch * 16 < (uint32_t)WIN ? nch * 16 : (uint32_t)WIN;  // bytes the window holds
+    auto rd = [&](uint32_t o) -> uint32_t {  // record byte o (o < len)
+        const uint32_t x = head + o;
+        return x < wvalid ? wbyte(row, x) : ld_byte_sync(my_a0 + o);
+    };
+    const Geom g = parse_geometry(rd, my_len, my_kind, MODE == MODE_EMIT);
+    const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
+    uint32_t st = g.st;
+    uint32_t ip_valid = 1, ip_ok = 1, l4_valid = 1, l4_ok = 1, partial = 0;
+    uint32_t ip_val = 0, l4_val = 0, fpos = 0, in_val = 0;
+    auto rsum = [&](uint32_t from, uint32_t to) -> uint32_t {  // record offsets
+        if (head + to <= wvalid) return region_sum(row, base, head + from, head + to);
+        uint32_t a = 0;  // slow path: straddles or leaves the window
+        for (uint32_t o = from; o < to; ++o) a += rd(o) << (8 * ((head + o) & 1));
+        return a;
+    };
+    if (g.fam == 4) {
+        uint32_t sh = rsum(g.ip_off, g.ip_off + g.ip_hl);
+        if (MODE == MODE_EMIT) {
+            const uint32_t f0 = rd(g.ip_off + 10), f1 = rd(g.ip_off + 11);
+            sh -= odd ? ((f0 << 8) + f1) : (f0 + (f1 << 8));
+        }
+        const uint32_t f = fold32(sh);
+        const uint32_t hdr = odd ? f : bswap16(f);  // == checksum::data(header)
+        if (MODE == MODE_EMIT) {
+            ip_val = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
+        } else {
+            ip_valid = hdr == 0xffffu;
+            ip_ok = caps_rx(p.caps_ipv4) ? ip_valid : 1u;
+        }
+    }
+    if (l4) {
+        fpos = g.l4_off + g.fo;
+        const uint32_t field = (rd(fpos) << 8) | rd(fpos + 1);
+        // L4 span sum = whole-buffer sum - [aligned start, l4_off) - [span_end, len)
+        uint32_t s = sum - rsum(0, g.l4_off) - (!EXACT && head ? region_sum(row, base, 0, head) : 0u);
+        if (g.span_end < my_len) s -= rsum(g.span_end, my_len);
+        auto word = [&](uint32_t v) { return odd ? v : bswap16(v); };  // BE u16 at an even offset
+        if (MODE == MODE_EMIT) {
+            s -= word(field);
+            if (g.in_off) {  // ICMPv4 error: the embedded IPv4 header first (csum_device.h)
+                uint32_t hin = 0;
+                for (uint32_t i = 0; i < g.in_hl / 2; ++i)
+                    if (i != 5) hin += (rd(g.in_off + 2 * i) << 8) | rd(g.in_off + 2 * i + 1);
+                in_val = caps_tx(p.caps_ipv4) ? (~fold32(hin) & 0xffffu) : 0u;
+                const uint32_t fi = g.in_off + 10;
+                s = s - word((rd(fi) << 8) | rd(fi + 1)) + word(in_val);
+            }
+        }
+        const uint32_t f = fold32(s);
+        const uint32_t dat = odd ? f : bswap16(f);  // == checksum::data(span)
+        const bool pseudo = g.proto == P_UDP || g.proto == P_TCP || g.proto == P_ICMP6;
+        uint32_t ph = 0;
+        if (pseudo) {
+            const uint32_t xa = fold32(rsum(g.addr_off, g.addr_off + 2 * g.addr_words));
+            const uint32_t addr = odd ? xa : bswap16(xa);  // canonical big-endian address sum
+            const uint32_t plen = g.proto == P_UDP ? (g.span_end - g.l4_off) : g.l4_len;
+            ph = fold32(addr + g.proto + (plen & 0xffffu));  // pseudo_header()
+        }
+        const uint32_t comb = pseudo ? fold32(ph + dat) : dat;  // combine()
+        uint32_t gate_caps;
+        switch (g.proto) {
+            case P_UDP: gate_caps = p.caps_udp; break;
+            case P_TCP: gate_caps = p.caps_tcp; break;
+            case P_ICMP4: gate_caps = p.caps_icmpv4; break;
+            case P_ICMP6: gate_caps = p.caps_icmpv6; break;
+            default: gate_caps = SMOL_CHECKSUM_NONE; break;  // IGMP
+        }
+        if (MODE == MODE_EMIT) {
+            const bool fill = g.proto == P_IGMP ? true : caps_tx(gate_caps);
+            uint32_t c = ~comb & 0xffffu;
+            if (g.proto == P_UDP && c == 0) c = 0xffffu;  // udp.rs:207
+            l4_val = fill ? c : 0u;
+        } else {
+            l4_valid = comb == 0xffffu;
+            if (g.proto == P_UDP && field == 0) l4_valid = 1;  // udp.rs:138-140
+            if (g.proto == P_UDP || g.proto == P_TCP) partial = ph == field;
+            l4_ok = caps_rx(gate_caps) ? l4_valid : 1u;
+        }
+    }
+    if (MODE == MODE_EMIT) {
+        if (g.fam == 4) store_be16((gu8)(my_a0 + g.ip_off + 10), ip_val);
+        if (g.in_off) store_be16((gu8)(my_a0 + g.in_off + 10), in_val);
+        if (l4) store_be16((gu8)(my_a0 + fpos), l4_val);
+        if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
+    } else {
+        const bool mal = (st & SMOL_ST_MALFORMED) != 0;
+        st |= (ip_ok ? SMOL_ST_IP_OK : 0u) | (l4_ok ? SMOL_ST_L4_OK : 0u) |
+              (partial ? SMOL_ST_L4_PARTIAL : 0u) | (ip_valid ? SMOL_ST_IP_VALID : 0u) |
+              (l4_valid ? SMOL_ST_L4_VALID : 0u) | ((ip_ok && l4_ok && !mal) ? SMOL_ST_ACCEPT : 0u);
+        ((gu8)p.status)[r] = (uint8_t)st;
+    }
+}
+
 // VAR: 0 = non-temporal record loads, 1 = plain loads (both on the record's 16-byte grid),
 // 2 = non-temporal loads on the record's 128-byte line grid (see csum_walk.h: nt loads need whole
 // lines; the chunks before the record are loaded and not summed).
@@ -273,109 +378,123 @@ __global__ __launch_bounds__(256) void csum_tile_kernel(KParams p) {
         wave_lds_sync();
 
         // ---- phase C: lane i finishes record i ----
+        if ((uint32_t)lane < cnt) finish_record<MODE, false>(p, &L.win[lane * WSTRIDE], L.sum[lane], my_a0, my_len, my_kind, r0 + lane);
+        wave_lds_sync();  // phase C's window reads complete before the next tile's phase B writes
+    }
+}
+
+
+#ifdef SMOL_EXP
+// ---------------------------------------------------------------------------------------------
+// Stripe kernel (experiments build; fixed-stride emit / verify over packed records of 1024..1520
+// bytes, natural grid).  Measured slower than the walk kernel: C2 verify
+// 0.264-0.268 against 0.242 ms, C4 0.315 against 0.210 ms, C2 emit 0.345 against 0.316 ms fresh —
+// the reads are faster, but one lane per record in phase C does the per-record work serially.
+//
+// A wavefront owns T = 8 consecutive records and reads their whole span (from the first record's
+// 128-byte line) as wave-contiguous 1-KiB pieces, NU per lane, all in flight at once: each load
+// instruction covers 8 consecutive lines of one place in the batch, where the walk kernel's covers
+// one line in each of 8 records.  Read-only probe over C2's 1.5 GB (tools/probe_pol.hip,
+// tools/probe_bw.hip): groups of 8 lanes over 2 steps 6.5 TB/s, one wave-wide step per record
+// 7.2 TB/s, 8-record stripes 7.1 TB/s.
+//
+// Phase B attributes each 16-byte chunk to the record holding its FIRST byte (a piece spans at most
+// two records, since stride >= 1024: the record of its first chunk and the next), keeps a running
+// sum for both, and reduces a record's sum over the wavefront when the pieces leave it.  The bytes
+// of a record's first chunk that follow its start (the chunk is attributed to the previous record)
+// are moved back in phase C from the record's window: + its own, - its successor's (a lane shuffle).
+// Bytes before the first record and past the last are masked.  Phase C is the tile kernel's.
+constexpr int STRIPE_T = 8;
+
+template <int MODE, int NU>
+__global__ __launch_bounds__(256) void csum_stripe_kernel(KParams p) {
+    constexpr int T = STRIPE_T;
+    __shared__ WaveLds<T> lds[4];
+    const int wave = (int)(threadIdx.x >> 6);
+    const int lane = (int)(threadIdx.x & 63);
+    WaveLds<T>& L = lds[wave];
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    const uint64_t dummy = (uint64_t)p.dummy;
+    const int32_t stride = (int32_t)p.stride;  // == len (packed), 1024 .. (NU * 1024 - 127) / T
+
+    for (uint64_t tile = logical_block(p.xcd_remap) * 4 + wave; tile * T < p.n; tile += nwaves) {
+        const uint64_t r0 = tile * T;
+        const uint32_t cnt = (uint32_t)((p.n - r0) < (uint64_t)T ? (p.n - r0) : (uint64_t)T);
+        const uint64_t a00 = (uint64_t)p.buf + r0 * p.stride;
+        const uint64_t S0 = a00 & ~127ull;
+        const int32_t h0 = (int32_t)(a00 - S0);
+        const int32_t end = (int32_t)cnt * stride;  // offsets relative to a00
+
+        // ---- phase B: the stripe, all pieces in flight ----
+        u32x4 v[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int32_t q = 1024 * u + 16 * lane - h0;  // the chunk's first byte, relative to a00
+            v[u] = ld16<true>((gcv4)(q < end && q + 16 > 0 ? S0 + 1024ull * u + 16ull * lane : dummy));
+        }
+        uint32_t cur = 0, nxt = 0;  // the sums of records ja and ja + 1 (this lane's part)
+        int32_t ja = h0 > 0 ? -1 : 0;       // the record of the piece's first byte (wave-uniform)
+        int32_t nb = (ja + 1) * stride;     // start of record ja + 1
+        auto flush = [&](int32_t jr, uint32_t x) {
+            const uint32_t tot = group_sum<64>(x);
+            if (lane == 0 && jr >= 0 && jr < (int32_t)cnt) L.sum[jr] = tot;
+        };
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int32_t o = 1024 * u - h0;  // the piece's first byte (uniform)
+            if (u > 0 && o >= nb) {           // the pieces have left record ja
+                flush(ja, cur);
+                cur = nxt;
+                nxt = 0;
+                ++ja;
+                nb += stride;
+            }
+            const int32_t q = o + 16 * lane;
+            u32x4 c = v[u];
+            uint32_t x;
+            if (o + 1024 > end && o < end + 16)  // the stripe's last bytes: mask past the end (uniform)
+                x = add_words(mask_dword(c.x, 0, end - q), add_words(mask_dword(c.y, 0, end - q - 4),
+                    add_words(mask_dword(c.z, 0, end - q - 8), add_words(mask_dword(c.w, 0, end - q - 12), 0u))));
+            else
+                x = add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u))));
+            if (u == 0 && q < 0) x = 0;  // before the first record (attributed to record -1)
+            const bool b = q >= nb;
+            cur += b ? 0u : x;
+            nxt += b ? x : 0u;
+            // the window rows: the chunks [w, w + WIN) of the record holding the chunk's last byte,
+            // w = the record's 16-byte boundary (relative to a00)
+            const int32_t jw = q + 15 >= nb ? ja + 1 : ja;
+            if (jw >= 0 && jw < (int32_t)cnt) {
+                const int32_t w = jw * stride - (int32_t)((a00 + (uint64_t)(jw * stride)) & 15u);
+                const int32_t k = q - w;
+                if (k >= 0 && k < WIN) {
+                    uint32_t* row = &L.win[jw * WSTRIDE + (k >> 2)];
+                    row[0] = c.x;
+                    row[1] = c.y;
+                    row[2] = c.z;
+                    row[3] = c.w;
+                }
+            }
+        }
+        flush(ja, cur);
+        flush(ja + 1, nxt);
+        wave_lds_sync();
+
+        // ---- phase C: lane i finishes record i ----
+        const uint64_t my_a0 = a00 + (uint64_t)lane * p.stride;
+        const uint32_t* row = &L.win[(lane < T ? lane : 0) * WSTRIDE];
+        const uint32_t hd = (uint32_t)(my_a0 & 15u);
+        // the bytes [a0, 16-byte boundary) of this record's first chunk, summed with record i - 1
+        const uint32_t xs = (lane < (int)cnt && hd) ? region_sum(row, my_a0 & ~15ull, hd, 16) : 0u;
+        const uint32_t xn = (uint32_t)__shfl_down((int)xs, 1, 64);
         if ((uint32_t)lane < cnt) {
-            const uint32_t* row = &L.win[lane * WSTRIDE];
-            const uint32_t head = (uint32_t)(my_a0 & 15u);
-            const uint64_t base = my_a0 & ~15ull;
-            const bool odd = (my_a0 & 1u) != 0;
-            const uint32_t nch = my_len ? (uint32_t)(((my_a0 + my_len + 15) >> 4) - (my_a0 >> 4)) : 0u;
-            const uint32_t wvalid = nch * 16 < (uint32_t)WIN ? nch * 16 : (uint32_t)WIN;  // bytes the window holds
-            auto rd = [&](uint32_t o) -> uint32_t {  // record byte o (o < len)
-                const uint32_t x = head + o;
-                return x < wvalid ? wbyte(row, x) : ld_byte_sync(my_a0 + o);
-            };
-            const Geom g = parse_geometry(rd, my_len, my_kind, MODE == MODE_EMIT);
-            const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
-            uint32_t st = g.st;
-            uint32_t ip_valid = 1, ip_ok = 1, l4_valid = 1, l4_ok = 1, partial = 0;
-            uint32_t ip_val = 0, l4_val = 0, fpos = 0, in_val = 0;
-            auto rsum = [&](uint32_t from, uint32_t to) -> uint32_t {  // record offsets
-                if (head + to <= wvalid) return region_sum(row, base, head + from, head + to);
-                uint32_t a = 0;  // slow path: straddles or leaves the window
-                for (uint32_t o = from; o < to; ++o) a += rd(o) << (8 * ((head + o) & 1));
-                return a;
-            };
-            if (g.fam == 4) {
-                uint32_t sh = rsum(g.ip_off, g.ip_off + g.ip_hl);
-                if (MODE == MODE_EMIT) {
-                    const uint32_t f0 = rd(g.ip_off + 10), f1 = rd(g.ip_off + 11);
-                    sh -= odd ? ((f0 << 8) + f1) : (f0 + (f1 << 8));
-                }
-                const uint32_t f = fold32(sh);
-                const uint32_t hdr = odd ? f : bswap16(f);  // == checksum::data(header)
-                if (MODE == MODE_EMIT) {
-                    ip_val = caps_tx(p.caps_ipv4) ? (~hdr & 0xffffu) : 0u;
-                } else {
-                    ip_valid = hdr == 0xffffu;
-                    ip_ok = caps_rx(p.caps_ipv4) ? ip_valid : 1u;
-                }
-            }
-            if (l4) {
-                fpos = g.l4_off + g.fo;
-                const uint32_t field = (rd(fpos) << 8) | rd(fpos + 1);
-                // L4 span sum = whole-buffer sum - [aligned start, l4_off) - [span_end, len)
-                uint32_t s = L.sum[lane] - rsum(0, g.l4_off) - (head ? region_sum(row, base, 0, head) : 0u);
-                if (g.span_end < my_len) s -= rsum(g.span_end, my_len);
-                auto word = [&](uint32_t v) { return odd ? v : bswap16(v); };  // BE u16 at an even offset
-                if (MODE == MODE_EMIT) {
-                    s -= word(field);
-                    if (g.in_off) {  // ICMPv4 error: the embedded IPv4 header first (csum_device.h)
-                        uint32_t hin = 0;
-                        for (uint32_t i = 0; i < g.in_hl / 2; ++i)
-                            if (i != 5) hin += (rd(g.in_off + 2 * i) << 8) | rd(g.in_off + 2 * i + 1);
-                        in_val = caps_tx(p.caps_ipv4) ? (~fold32(hin) & 0xffffu) : 0u;
-                        const uint32_t fi = g.in_off + 10;
-                        s = s - word((rd(fi) << 8) | rd(fi + 1)) + word(in_val);
-                    }
-                }
-                const uint32_t f = fold32(s);
-                const uint32_t dat = odd ? f : bswap16(f);  // == checksum::data(span)
-                const bool pseudo = g.proto == P_UDP || g.proto == P_TCP || g.proto == P_ICMP6;
-                uint32_t ph = 0;
-                if (pseudo) {
-                    const uint32_t xa = fold32(rsum(g.addr_off, g.addr_off + 2 * g.addr_words));
-                    const uint32_t addr = odd ? xa : bswap16(xa);  // canonical big-endian address sum
-                    const uint32_t plen = g.proto == P_UDP ? (g.span_end - g.l4_off) : g.l4_len;
-                    ph = fold32(addr + g.proto + (plen & 0xffffu));  // pseudo_header()
-                }
-                const uint32_t comb = pseudo ? fold32(ph + dat) : dat;  // combine()
-                uint32_t gate_caps;
-                switch (g.proto) {
-                    case P_UDP: gate_caps = p.caps_udp; break;
-                    case P_TCP: gate_caps = p.caps_tcp; break;
-                    case P_ICMP4: gate_caps = p.caps_icmpv4; break;
-                    case P_ICMP6: gate_caps = p.caps_icmpv6; break;
-                    default: gate_caps = SMOL_CHECKSUM_NONE; break;  // IGMP
-                }
-                if (MODE == MODE_EMIT) {
-                    const bool fill = g.proto == P_IGMP ? true : caps_tx(gate_caps);
-                    uint32_t c = ~comb & 0xffffu;
-                    if (g.proto == P_UDP && c == 0) c = 0xffffu;  // udp.rs:207
-                    l4_val = fill ? c : 0u;
-                } else {
-                    l4_valid = comb == 0xffffu;
-                    if (g.proto == P_UDP && field == 0) l4_valid = 1;  // udp.rs:138-140
-                    if (g.proto == P_UDP || g.proto == P_TCP) partial = ph == field;
-                    l4_ok = caps_rx(gate_caps) ? l4_valid : 1u;
-                }
-            }
-            const uint64_t r = r0 + lane;
-            if (MODE == MODE_EMIT) {
-                if (g.fam == 4) store_be16((gu8)(my_a0 + g.ip_off + 10), ip_val);
-                if (g.in_off) store_be16((gu8)(my_a0 + g.in_off + 10), in_val);
-                if (l4) store_be16((gu8)(my_a0 + fpos), l4_val);
-                if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
-            } else {
-                const bool mal = (st & SMOL_ST_MALFORMED) != 0;
-                st |= (ip_ok ? SMOL_ST_IP_OK : 0u) | (l4_ok ? SMOL_ST_L4_OK : 0u) |
-                      (partial ? SMOL_ST_L4_PARTIAL : 0u) | (ip_valid ? SMOL_ST_IP_VALID : 0u) |
-                      (l4_valid ? SMOL_ST_L4_VALID : 0u) | ((ip_ok && l4_ok && !mal) ? SMOL_ST_ACCEPT : 0u);
-                ((gu8)p.status)[r] = (uint8_t)st;
-            }
+            const uint32_t sum = L.sum[lane] + xs - ((uint32_t)lane + 1 < cnt ? xn : 0u);
+            finish_record<MODE, true>(p, row, sum, my_a0, p.len, p.kind, r0 + lane);
         }
         wave_lds_sync();  // phase C's window reads complete before the next tile's phase B writes
     }
 }
+#endif
 
 template <int G, int U, int MODE, bool IMPLICIT, int VAR, int TILE>
 static hipError_t launch_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
@@ -430,6 +549,30 @@ static hipError_t launch_mode(int shape, int var, const KParams& p, uint32_t max
 }
 
 }  // namespace tile
+
+// The stripe kernel serves fixed-stride batches of packed records (stride == len) of 1024 .. 1520
+// bytes over a natural grid; false: not this batch.
+bool stripe_fits(const KParams& p) {
+#ifdef SMOL_EXP
+    return p.desc == nullptr && p.len == p.stride && p.len >= 1024 && p.len <= (12 * 1024 - 127) / tile::STRIPE_T;
+#else
+    return false;
+#endif
+}
+
+hipError_t launch_stripe(int mode, const KParams& p, hipStream_t s) {
+#ifdef SMOL_EXP
+    const uint64_t blocks = (p.n + 4 * tile::STRIPE_T - 1) / (4 * tile::STRIPE_T);
+    const uint32_t b = grid_blocks(blocks, 0x7fffffff);
+    note_launch(KERN_TILE, 42, 64, 12);
+    if (mode == MODE_EMIT) hipLaunchKernelGGL((tile::csum_stripe_kernel<MODE_EMIT, 12>), dim3(b), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((tile::csum_stripe_kernel<MODE_VERIFY, 12>), dim3(b), dim3(256), 0, s, p);
+    return hipGetLastError();
+#else
+    (void)mode, (void)p, (void)s;
+    return hipErrorInvalidValue;
+#endif
+}
 
 hipError_t launch_tile(int mode, int shape, int var, int tile_records, const KParams& p, uint32_t max_blocks,
                        hipStream_t s) {

@@ -209,10 +209,10 @@ def test_copy_emit_mixed_packed(eng, shape, variant):
 
 @pytest.mark.parametrize("variant", [-1, 16, 17, 21])
 def test_copy_emit_packed_zero_gaps(eng, variant):
-    eng.need(variant)
     """C3-style batch: TCP records of U[64, 9000] bytes packed back to back with no gap (odd
     offsets), so neighbouring records share cache lines.  Copy-emit rewrites every byte of a record
     (include/smolcsum.h, INTEGRATION.md §4.1.1); a neighbour's bytes must survive bit for bit."""
+    eng.need(variant)
     rng = np.random.default_rng(17)
     recs, spec = [], []
     for i in range(1500):
@@ -228,8 +228,8 @@ def test_copy_emit_packed_zero_gaps(eng, variant):
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 def test_copy_emit_all_alignments(eng, variant):
-    eng.need(variant)
     """dst offsets and source offsets cover every residue mod 16."""
+    eng.need(variant)
     rng = np.random.default_rng(7)
     recs, spec = [], []
     for i in range(512):
@@ -300,10 +300,10 @@ def test_copy_emit_errors(eng):
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 def test_copy_emit_far_fields(eng, variant):
-    eng.need(variant)
     """IPv6 records whose Hop-by-Hop header pushes the TCP / UDP checksum field past the 128-B
     header window (or across its edge): the field must still be the emitted value, whether the copy
     range covers it or not, at every record alignment."""
+    eng.need(variant)
     rng = np.random.default_rng(21)
     recs, spec = [], []
     for i in range(600):
@@ -335,9 +335,9 @@ def test_copy_emit_far_fields(eng, variant):
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
 def test_copy_emit_tiny_records(eng, variant):
-    eng.need(variant)
     """Records of 0 .. 47 bytes (shorter than the header window, than one 16-B chunk, or empty)
     packed at odd offsets, with copy ranges anywhere inside them (or not fitting)."""
+    eng.need(variant)
     rng = np.random.default_rng(33)
     recs, spec = [], []
     for i in range(900):
@@ -356,11 +356,11 @@ def test_copy_emit_tiny_records(eng, variant):
 
 @pytest.mark.parametrize("variant", [-1, 16, 17, 21])
 def test_copy_emit_packed_fields_in_last_line(eng, variant):
-    eng.need(variant)
     """Records packed back to back (no gaps) where some hold their L4 checksum field in their last
     128-B line (an IPv6 Hop-by-Hop header of 256-2000 B before a short TCP / UDP segment), between
     ordinary ones: the fields and the neighbours' bytes, which share those lines, must come out
     exactly as memcpy + emit leaves them."""
+    eng.need(variant)
     rng = np.random.default_rng(41)
     recs, spec = [], []
     for i in range(1500):

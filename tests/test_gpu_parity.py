@@ -630,10 +630,10 @@ def _expected_launch(variant, op, has_desc):
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 13, 19, 23, 24, 25, 26, 27, 28, 29, 37, 38, 39])
 def test_variants_fixed_stride(eng, variant):
-    eng.need(variant)
     """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
     the oracle on fixed-stride batches: strides equal to the record length (neighbours share
     lines), odd strides, gaps, every shape, natural and persistent grids."""
+    eng.need(variant)
     for profile, kind, L in [(E.SYNTH_UDP4, E.KIND_IP, 1500), (E.SYNTH_V6MIX, E.KIND_IP, 1320),
                              (E.SYNTH_TCP4, E.KIND_IP, 97), (E.SYNTH_ETH_TCP4, E.KIND_ETH, 1514),
                              (E.SYNTH_UDP4, E.KIND_IP, 128), (E.SYNTH_TCP4, E.KIND_IP, 4000)]:
@@ -670,6 +670,60 @@ def test_variants_fixed_stride(eng, variant):
                     assert np.array_equal(st, ref_v), (variant, L, stride, shape, blocks)
                     assert np.array_equal(got, ref_e), (variant, L, stride, shape, blocks)
                     assert np.array_equal(est.cpu().numpy(), ref_es)
+
+
+def test_stripe_kernel(eng):
+    """The stripe kernel (variant 42: packed fixed-stride records of 1024-1520 bytes, a wavefront
+    streams 8 records as wave-contiguous 1-KiB pieces) against the oracle: every profile, odd record
+    lengths (odd starts), batch sizes that leave a partial last wavefront, 1/7 corrupted, caps
+    variants; the whole buffer is compared after emit.  Batches it does not serve (gapped strides,
+    other lengths, descriptor batches) fall back to the walk kernel."""
+    eng.need(42)
+    for profile, kind, L in [(E.SYNTH_UDP4, E.KIND_IP, 1500), (E.SYNTH_UDP4, E.KIND_IP, 1024),
+                             (E.SYNTH_V6MIX, E.KIND_IP, 1320), (E.SYNTH_TCP4, E.KIND_IP, 1499),
+                             (E.SYNTH_ETH_TCP4, E.KIND_ETH, 1514), (E.SYNTH_TCP4, E.KIND_IP, 1025),
+                             (E.SYNTH_V6MIX, E.KIND_IP, 1519), (E.SYNTH_UDP4, E.KIND_IP, 1520)]:
+        for n, off in ((1, 0), (7, 3), (8, 0), (9, 64), (257, 1), (4099, 17)):
+            host = np.zeros(off + n * L + 128, dtype=np.uint8)
+            tmp = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+            batch = E.Batch.fixed(n, L, L, kind)
+            eng.synth(tmp, batch, profile, seed=L * 3 + n)
+            eng.emit(tmp, batch)
+            eng.corrupt(tmp, batch, every=7, seed=n)
+            host[off:off + tmp.numel()] = tmp.cpu().numpy()
+            for caps in (CAPS_DEFAULT, (2, 3, 0, 1, 0)):
+                d = torch.from_numpy(host.copy()).cuda()
+                view = d[off:]
+                eng.set_variant(42)
+                try:
+                    st = eng.verify(view, batch, caps=caps).cpu().numpy()
+                    lv = eng.last_launch()
+                    eng.emit(view, batch, caps=caps)
+                    le = eng.last_launch()
+                finally:
+                    eng.set_variant(-1)
+                assert (lv["kernel"], lv["variant"]) == ("csum_tile_kernel", 42), lv
+                assert (le["kernel"], le["variant"]) == ("csum_tile_kernel", 42), le
+                ref_v = oracle.batch_verify(host[off:].copy(), None, n, L, L, kind, caps)
+                assert np.array_equal(st, ref_v), (L, n, off, caps, np.nonzero(st != ref_v)[0][:8])
+                ref_e = host.copy()
+                oracle.batch_emit(ref_e[off:], None, n, L, L, kind, caps)
+                got = d.cpu().numpy()
+                assert np.array_equal(got, ref_e), (L, n, off, caps, np.nonzero(got != ref_e)[0][:8])
+    # not served: gapped stride, a length outside 1024-1520 -> the walk kernel
+    for L, stride in ((1500, 1501), (1000, 1000), (1600, 1600)):
+        n = 100
+        buf = torch.zeros(n * stride + 64, dtype=torch.uint8, device="cuda:0")
+        batch = E.Batch.fixed(n, stride, L, E.KIND_IP)
+        eng.synth(buf, batch, E.SYNTH_UDP4, seed=L)
+        host = buf.cpu().numpy().copy()
+        eng.set_variant(42)
+        try:
+            st = eng.verify(buf, batch).cpu().numpy()
+            assert eng.last_launch()["kernel"] == "csum_kernel"
+        finally:
+            eng.set_variant(-1)
+        assert np.array_equal(st, oracle.batch_verify(host, None, n, stride, L, E.KIND_IP, CAPS_DEFAULT))
 
 
 def test_pretty_print_annotations(eng, golden):

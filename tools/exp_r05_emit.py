@@ -4,7 +4,7 @@ batches in turn (every emit a batch its previous pass did not just write, as the
 do since round 5), interleaved rounds on one box.  Verify of the RX batch is timed in the same
 rounds as the reference.  Store variants must leave the bytes of the first variant listed; `| 64`
 variants (experiments: stores compiled out) are timing only.
-Usage: [VARS=29,5,31,32] [K=32] [ROUNDS=4] exp_r05_emit.py [c2,c4]"""
+Usage: [VARS=29,5,31,32] [VVARS=-1,13 (verify variants)] [K=32] [ROUNDS=4] exp_r05_emit.py [c2,c4]"""
 import json
 import os
 import sys
@@ -69,9 +69,11 @@ def main():
 
     for rnd in range(int(os.environ.get("ROUNDS", "4"))):
         for c, wl in wls.items():
-            eng.set_variant(-1)
-            ver = timed(lambda j: eng.verify(wl.rxs[j], wl.batch, status=wl.status))
-            print(json.dumps({"round": rnd, "cfg": c, "variant": "verify", "ms": round(ver, 4)}), flush=True)
+            for vv in [int(x) for x in os.environ.get("VVARS", "-1").split(",")]:
+                eng.set_variant(vv)
+                ver = timed(lambda j: eng.verify(wl.rxs[j], wl.batch, status=wl.status))
+                name = "verify" if vv < 0 else f"verify{vv}"
+                print(json.dumps({"round": rnd, "cfg": c, "variant": name, "ms": round(ver, 4)}), flush=True)
             for v in vars_:
                 eng.set_variant(v)
                 fresh = timed(lambda j: eng.emit(wl.txs[j], wl.batch))

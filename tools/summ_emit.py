@@ -10,7 +10,7 @@ agg = collections.defaultdict(list)
 for r in rows:
     if r.get("round", 0) > 0:
         k = (r["cfg"], str(r["variant"]))
-        agg[k].append((r["ms"],) if r["variant"] == "verify" else (r["emit_fresh_ms"], r["emit_same_ms"]))
+        agg[k].append((r["ms"],) if str(r["variant"]).startswith("verify") else (r["emit_fresh_ms"], r["emit_same_ms"]))
 for (c, v), xs in sorted(agg.items()):
     cols = list(zip(*xs))
     print(c, v.rjust(6), "  ".join("%s %.4f-%.4f" % (n, min(col), max(col)) for n, col in zip(("fresh", "same"), cols)))
