@@ -503,6 +503,11 @@ def cpu_baseline(E, wl, seconds: float):
     return out, parity
 
 
+def _launch_name(ll):
+    """'xwalk_kernel v47 G8 U2' from an engine.last_launch() record."""
+    return "?" if not ll else f"{ll['kernel']} v{ll['variant']} G{ll['G']} U{ll['U']}"
+
+
 def load_traffic(cfg: str, kernel: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/*traffic*.json)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
@@ -610,6 +615,7 @@ def main(argv=None):
     stream = torch.cuda.current_stream(dev)
     R = len(wl.txs)
     nstep = [0]
+    launched = {}  # the kernel each op ran (smol_csum_tool_last_launch), recorded at instrumented steps
 
     def step(ev=None, same=False):
         # step i emits TX batch i mod R and verifies RX batch i mod R (same: batch 0 every time)
@@ -622,9 +628,11 @@ def main(argv=None):
         else:
             eng.emit(wl.txs[j], wl.batch, stream=stream)
         if ev is not None:
+            launched["copy_emit" if wl.copy is not None else "emit"] = eng.last_launch()
             ev[1].record(stream)
         eng.verify(wl.rxs[j], wl.batch, status=wl.status, stream=stream)
         if ev is not None:
+            launched["verify"] = eng.last_launch()
             ev[2].record(stream)
 
     # Clock ramp: a freshly idle MI355X takes ~15 ms of sustained load before its kernels run at
@@ -798,11 +806,12 @@ def main(argv=None):
             "config": {"workload": wl.workload, "records_per_gpu": wl.n, "parallelism": f"shard x{world} (no collective)",
                        "checksummed_bytes_per_step_per_gpu": 2 * wl.span_bytes,
                        "process_group": dist.get_backend() if pg else None},
-            "roofline": {"bound": "hbm", "kernel": f"{eng.kernel_name(dop, wl.desc_bytes > 0)} ({dop})", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": f"{_launch_name(launched.get(dop))} ({dop})", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": tsrc,
                          "algorithmic_bytes_per_launch": kd["bytes"], "launch_ms": round(kd["ms"], 4)},
             "kernels_ms": {k: round(v["ms"], 4) for k, v in kernels.items()},
+            "kernels_launched": {k: _launch_name(v) for k, v in launched.items()},
             "kernels_roofline": {k: {"algorithmic_bytes_per_launch": v["bytes"], "launch_ms": round(v["ms"], 4),
                                      "achieved_GBs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1),
                                      "frac": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}

@@ -103,6 +103,21 @@ int walk_variant(int mode, bool has_desc) {
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
+// Round 5: the transposed walk (csum_xwalk.hip, variant 47: emit with whole field segments) for packed
+// fixed-stride records where it beats the walk kernel.  Verify and emit of synthetic IPv4/UDP over
+// ~1.5 GB, R = 4 batches in turn, one box (tools/exp_r05_vlen.py, profiles/r05_experiments/
+// xwalk_lengths.jsonl), walk -> transposed walk in TB/s: verify 1500 B 6.41 -> 6.65, 1760 B 4.34 ->
+// 6.98, 2500 B 2.89 -> 6.45, 3969 B 4.43 -> 6.73, 5000 B 4.65 -> 6.42, 8065 B 6.51 -> 6.65, and
+// slower at 1024 / 1320 B (6.13 / 6.67 -> 5.29 / 6.33) and from 9000 B (6.44 -> 6.27); emit
+// 1500 B 4.99 -> 4.77 (slower), 1760 B 3.35 -> 5.41, 2500 B 2.59 -> 5.36, 9000 B 5.66 -> 6.22,
+// 12000 B 6.18 -> 6.07.
+bool xwalk_auto(int mode, const smol_csum_batch_t* b) {
+    if (b->desc || b->stride != b->len) return false;
+    if (mode == MODE_VERIFY) return b->len >= 1473 && b->len <= 8065;
+    if (mode == MODE_EMIT) return b->len >= 1666 && b->len <= 10000;
+    return false;
+}
+
 // The XCD block order (csum_launch.h xcd_block / xcd_chunk) when none is forced: the contiguous order
 // for fixed-stride emit over at least 4 GiB.  Measured per 2^20 C2 records (tools/exp_inplace.py, one box,
 // profiles/r04_experiments/xcd_remap.jsonl): emit 0.327 -> 0.298 ms at 2^22 records (6.3 GB),
@@ -123,21 +138,22 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
+    if (variant == 47) return 44;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
 
 // The kernel variants this build runs (smol_csum_tool_variant_built).  The product library: the
-// defaults (walk 5 / 13 / 39, tile 7, copy 21) and one fallback each (copy 17; walk 5 and 13 serve
-// each other).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
+// defaults (walk 5 / 13 / 39, transposed walk 47, tile 7, copy 21) and one fallback each (copy 17;
+// walk 5 and 13 serve each other; 44 = 47 with 2-B field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
 bool variant_built(int v) {
     switch (v) {
-        case -1: case 5: case 7: case 13: case 17: case 21: case 39: return true;
+        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 47: return true;
         default: break;
     }
 #ifdef SMOL_EXP
     const int b = v >= 64 ? v - 64 : v;
-    if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39);
+    if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
            (v >= 31 && v <= 38) || v == 42;
 #else
@@ -214,11 +230,15 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     // run variant 0 for it).
     int variant = ctx->variant;
     const bool has_desc = b->desc != nullptr;
-    if (variant < 0) variant = auto_variant(mode, has_desc);
+    if (variant < 0) variant = (!d_addrs && xwalk_auto(mode, b)) ? 47 : auto_variant(mode, has_desc);
     if (mode == MODE_EMIT && (b->flags & SMOL_BATCH_FIELD_STORES)) variant = field_store_variant(variant, has_desc);
     // the stripe kernel (variant 42) serves emit / verify of packed fixed-stride records of 1024-1520 B
     const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
     if (variant == 42 && !stripe) variant = walk_variant(mode, has_desc);
+    // the transposed walk (variants 44 / 47, 64 + 44 / 47): packed records of 1024 - 16257 B
+    const bool xw_var = variant % 64 == 44 || variant % 64 == 47;
+    const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
+    if (xw_var && !xwalk) variant = walk_variant(mode, has_desc);
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
     if (tile_var && (mode == MODE_DATA || mode == MODE_COPY || d_addrs)) variant = walk_variant(mode, has_desc);
     const bool use_tile = variant == 3 || variant == 4 || variant == 7;
@@ -253,6 +273,11 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         const int cshape = ctx->shape >= 0 ? ctx->shape : ((var == 17 || var == 21) ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
+        return SMOL_OK;
+    }
+    if (xwalk) {
+        hipError_t e = launch_xwalk(mode, variant, p, s);
+        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         return SMOL_OK;
     }
     if (stripe) {

@@ -86,7 +86,7 @@ __device__ inline uint64_t logical_block(uint32_t xcd_remap) {
 // The kernel instantiation of the process's last checksum launch, packed kernel << 24 | variant << 16
 // | G << 8 | U (smol_csum_tool_last_launch): tests check that a forced variant runs the kernel it
 // names rather than a dispatch fallback.
-enum { KERN_WALK = 1, KERN_TILE = 2, KERN_COPY = 3, KERN_WALK_NHC = 4 };
+enum { KERN_WALK = 1, KERN_TILE = 2, KERN_COPY = 3, KERN_WALK_NHC = 4, KERN_XWALK = 5 };
 inline std::atomic<uint32_t> g_last_launch{0};
 inline void note_launch(uint32_t kern, uint32_t var, uint32_t g, uint32_t u) {
     g_last_launch.store(kern << 24 | (var & 0xffu) << 16 | (g & 0xffu) << 8 | (u & 0xffu),
@@ -120,6 +120,10 @@ hipError_t launch_tile(int mode, int shape, int var, int tile_records, const KPa
 // Stripe kernel (csum_tile.hip, variant 42): fixed-stride packed records of 1024-1520 bytes.
 bool stripe_fits(const KParams& p);
 hipError_t launch_stripe(int mode, const KParams& p, hipStream_t s);
+// Transposed walk (csum_xwalk.hip, variants 44 / 47 = whole field segments): fixed-stride packed
+// records of 1024-16257 bytes.
+bool xwalk_fits(const KParams& p);
+hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s);
 
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
 struct SynthParams {

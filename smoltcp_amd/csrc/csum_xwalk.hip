@@ -1,0 +1,285 @@
+// Transposed walk (variants 44 / 47): fixed-stride emit / verify of packed
+// records of 1024 .. 16257 bytes over a natural grid, with the walk kernel's per-record work (a group
+// of G lanes parses and finishes one record, R = 64 / G records per wavefront) and a different load
+// mapping.
+//
+// The walk kernel's load instruction covers one 128-B line in each of the wavefront's 8 records
+// (8 lanes per record); here load instruction (s, j) covers 1 KiB of ONE record: chunks
+// 64 s .. 64 s + 63 of record j, one per lane, NS = 16 / R instructions per record.  A read-only probe
+// of the two patterns over C2's 1.5 GB (tools/probe_pol.hip, profiles/r05_experiments/
+// read_shape_probe.txt): 6.5 TB/s for the walk's (8 lanes, 2 steps), 7.2 TB/s for a whole wavefront
+// per record in one step.  All 16 loads of a wavefront are issued at once, as buffer loads: one
+// resource per wavefront based at its first record's line, record j's line offset as the scalar
+// offset, the chunk as the lane's offset; a chunk past the record's loads gets an offset past the
+// resource's range, which returns 0 without a memory access.  R by record length: 8 up to 1921 B,
+// 4 up to 3969 B, 2 up to 8065 B, 1 up to 16257 B.
+//
+// Sums.  A lane adds its chunk of record j to its accumulator j (j is a compile-time index), and a
+// reduce-scatter over the wavefront (exchanges across 32, 16, .., G lanes, then the group's own
+// reduction) leaves record j's sum in group j.  Chunks are summed whole where that is exact and
+// corrected in the finish from the LDS windows:
+//  - the bytes of a record's first line before its start belong to the previous record:
+//    subtracted (hs_j, from record j's window) and, when the previous record is in this wavefront,
+//    added to that record, which does not load the line (the line holding record j + 1's first
+//    byte is loaded once, as record j + 1's first chunk: csum_walk.h shared_from);
+//  - a record whose checksummed span ends before its end (UDP length < the IP payload, malformed or
+//    unsupported records), and the wavefront's last record (its last line is the next wavefront's),
+//    mask every chunk to [0, span_end) instead (the walk's masked sum).
+//
+// Measured (profiles/r05_experiments/xwalk_*.txt): the other forms tried, a 64-bit-address load from
+// the dummy line for out-of-range chunks, a persistent grid (one wavefront steps over the batch 8
+// records at a time) and 5 wavefronts per SIMD (96 VGPRs), were all slower.
+#include "csum_walk.h"
+
+namespace smolcsum {
+
+namespace xwalk {
+
+constexpr int WIN_CH = 16;  // the LDS window: 256 B from the record's 128-B line
+constexpr int WAVES = 4;    // wavefronts per workgroup
+
+// Sum of the words of `c` with record offsets in [0, hi) (pos: the chunk's first byte, relative to
+// the record start).
+__device__ __forceinline__ uint32_t span_sum(const u32x4& c, int pos, int hi) {
+    if (pos >= 0 && pos + 16 <= hi) return add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u))));
+    return sum_masked_words(c, -pos, hi - pos, 0u);
+}
+
+// The value of lane ^ H (H = 32 / 16 / 8 / ..: across the wavefront, a 32-lane half, a row)
+template <int H>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+    if constexpr (H == 32) return (uint32_t)__shfl_xor((int)v, 32, 64);
+    else if constexpr (H == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+    else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+}
+
+// Reduce-scatter of acc[0 .. N) over the lanes of bit H and below down to G: record j's partial sums
+// end in the lanes with (lane / G) % (N) == j.
+template <int N, int H>
+__device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) {
+    if constexpr (N == 1) {
+        return acc[0];
+    } else {
+        const bool up = (wl & H) != 0;
+        uint32_t a[N / 2];
+#pragma unroll
+        for (int i = 0; i < N / 2; ++i) {
+            const uint32_t keep = up ? acc[i + N / 2] : acc[i];
+            const uint32_t send = up ? acc[i] : acc[i + N / 2];
+            a[i] = keep + lane_xor<H>(send);
+        }
+        return reduce_scatter<N / 2, H / 2>(a, wl);
+    }
+}
+
+}  // namespace xwalk
+
+// SEG (variant 47; emit): the 64-B segments that hold a record's fields go out whole from its LDS
+// window, the fields patched in (csum_walk.h variant 38's decision, the wavefront's groups all on
+// their one record): a whole segment costs HBM a plain write where a 2-B store costs a
+// read-modify-write.  NOSTORE (variant 64 + v): emit computes every field value and stores none.
+template <int MODE, int R, bool NOSTORE, bool SEG>
+__global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
+    using namespace xwalk;
+    constexpr bool EMIT = MODE == MODE_EMIT;
+    constexpr int G = 64 / R;    // lanes per record
+    constexpr int NS = 16 / R;   // load instructions (1 KiB each) per record
+    constexpr int GPB = WAVES * R;
+    __shared__ u32x4 win[GPB][WIN_CH];
+    __shared__ uint32_t spanbuf[GPB];
+    const int wl = (int)(threadIdx.x & 63);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform: scalar offsets
+    const int lane = wl & (G - 1);
+    const int gw = wl / G;  // the group (record) within the wavefront
+    const int gib = wv * R + gw;
+    const uint64_t rw0 = (logical_block(p.xcd_remap) * WAVES + (uint64_t)wv) * R;  // the wavefront's first record
+    if (rw0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)(p.n - rw0 < (uint64_t)R ? p.n - rw0 : (uint64_t)R);
+    const uint32_t len = p.len;
+    const uint64_t stride = p.stride;
+
+    // ---- all loads of the wavefront's records (record j: chunks below nload_j of its line grid) ----
+    u32x4 v[NS][R];
+    uint32_t head[R], nload[R];
+    const uint64_t wbase = ((uint64_t)p.buf + rw0 * stride) & ~127ull;
+    const uint32_t whi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wbase >> 32));
+    const uint32_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wbase);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)whi << 32) | wlo), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const uint64_t a0 = (uint64_t)p.buf + (rw0 + (uint64_t)j) * stride;
+        const uint64_t b = a0 & ~127ull;
+        head[j] = (uint32_t)(a0 - b);
+        const uint32_t nch = (uint32_t)j < cnt ? (uint32_t)(((a0 + len + 15) >> 4) - (b >> 4)) : 0u;
+        // the line holding record j + 1's first byte is record j + 1's to load
+        const bool shared = (uint32_t)j + 1 < cnt;
+        nload[j] = shared ? (uint32_t)((((a0 + stride) & ~127ull) - b) >> 4) : nch;
+        const int soff = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b - wbase));
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const uint32_t k = (uint32_t)(64 * s + wl);
+            v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, k < nload[j] ? 16u * k : 0x80000000u, soff, 2 /* nt */);
+        }
+    }
+    // ---- the windows: chunks 0 .. 15 of record j are lanes 0 .. 15 of load (0, j) ----
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (wl < WIN_CH && (uint32_t)j < cnt) win[wv * R + j][wl] = v[0][j];
+    wave_lds_sync();
+
+    const bool mine = (uint32_t)gw < cnt;
+    const uint64_t r = rw0 + (uint64_t)gw;
+    const uint64_t a0 = (uint64_t)p.buf + r * stride;
+    const uint32_t hd = (uint32_t)(a0 & 127u);
+    const uint8_t* winb = reinterpret_cast<const uint8_t*>(&win[gib][0]);
+    auto rd = [&](uint32_t o) -> uint32_t {
+        const uint32_t x = hd + o;
+        if (x < 16u * WIN_CH) return (uint32_t)winb[x];
+        return ld_byte_sync(a0 + o);
+    };
+    Geom g = Geom{};
+    if (mine) g = parse_geometry<false>(rd, len, p.kind, EMIT);
+    const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
+    const int s1 = mine && l4 ? (int)g.span_end : 0;
+    // hs: the bytes of this record's first line before its start (window bytes [0, hd)), as
+    // aligned words; lane i takes window chunks i, i + G, ..
+    uint32_t hs = 0;
+#pragma unroll
+    for (int c = 0; c < WIN_CH; c += G)
+        if (c + lane < WIN_CH) hs = sum_masked_words(win[gib][c + lane], 0, (int)hd - 16 * (c + lane), hs);
+    hs = group_sum<G>(hs);
+    if (lane == 0) spanbuf[gib] = (uint32_t)s1;
+    wave_lds_sync();
+    int span[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) span[j] = (int)spanbuf[wv * R + j];
+
+    // ---- sums: accumulator j of every lane holds its chunks of record j ----
+    uint32_t acc[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        acc[j] = 0;
+        // whole chunks: the span runs to the record's end and the next record takes the last line
+        const bool whole = (uint32_t)j + 1 < cnt && span[j] == (int)len;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const uint32_t k = (uint32_t)(64 * s + wl);
+            const u32x4 c = v[s][j];
+            uint32_t x;
+            if (whole) x = add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u))));
+            else x = span_sum(c, 16 * (int)k - (int)head[j], span[j]);
+            acc[j] += k < nload[j] ? x : 0u;
+        }
+    }
+    // ---- reduce-scatter: record j's sum to group j ----
+    uint32_t tot = group_sum<G>(reduce_scatter<R, 32>(acc, wl));
+    // corrections: the first line's bytes before the record (whole-chunk records only), and the
+    // last line's bytes of this record that record j + 1 loaded (its hs)
+    const uint32_t hs_next = (uint32_t)__shfl_down((int)hs, G, 64);
+    const bool whole = (uint32_t)gw + 1 < cnt && s1 == (int)len;
+    if (whole) {
+        tot = tot - hs + hs_next;
+    } else if ((uint32_t)gw + 1 < cnt) {
+        // masked sums: the first line's extra bytes were masked out; the bytes record j + 1 loaded
+        // are record offsets [len - hdn, len) = its window's bytes [0, hdn), counted below the
+        // span's end
+        const uint32_t hdn = (uint32_t)((a0 + stride) & 127u);
+        const int lim = min((int)hdn, s1 - ((int)len - (int)hdn));
+        uint32_t t = 0;
+#pragma unroll
+        for (int c = 0; c < WIN_CH; c += G)
+            if (c + lane < WIN_CH) t = sum_masked_words(win[gib + 1][c + lane], 0, lim - 16 * (c + lane), t);
+        tot += group_sum<G>(t);
+    }
+    // ---- finish: the walk kernel's gates (lane 0 writes) ----
+    if constexpr (EMIT && SEG) {
+        // A segment that starts before the record also holds record r-1's last bytes: whole only
+        // when r-1 has no field in its last 64 bytes (its group says so: ok_tail) and r-1 is in this
+        // wavefront.  A record whose fields end 64 bytes or more before its end never reaches into
+        // r+1 with its own segments.
+        uint32_t f[3], lo = NO_FIELD, hi = 0;
+        emit_fields(g, f);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (f[i] != NO_FIELD) {
+                lo = f[i] < lo ? f[i] : lo;
+                hi = f[i] + 2 > hi ? f[i] + 2 : hi;
+            }
+        const bool ok_tail = hi == 0 || hi + 64 <= len;
+        const uint64_t okm = __ballot(lane == 0 && mine && ok_tail);
+        uint64_t wsA = ~0ull, wsB = ~0ull;
+        if (mine && (g.fam == 4 || g.fam == 6) && hi != 0 && ok_tail) {
+            const bool prev_ok = gw != 0 && ((okm >> (wl - lane - G)) & 1ull);
+            const int32_t ph = (int32_t)(a0 & 63u);
+            const int32_t rA = ((ph + (int32_t)lo) & ~63) - ph, rB = ((ph + (int32_t)hi - 1) & ~63) - ph;
+            const int32_t wend = 16 * WIN_CH - (int32_t)hd;
+            auto whole_seg = [&](int32_t rel) { return rB <= rA + 64 && rel + 64 <= wend && (rel >= 0 || prev_ok); };
+            if (whole_seg(rA)) wsA = a0 + (int64_t)rA;
+            if (rB != rA && whole_seg(rB)) wsB = a0 + (int64_t)rB;
+        }
+        uint8_t* winw = reinterpret_cast<uint8_t*>(&win[gib][0]);
+        if (mine)
+            finish_gates<G, MODE, false, decltype(rd), 16 * WIN_CH, true, NOSTORE>(
+                p, g, lane == 0 ? tot : 0u, rd, winb, hd, a0, r, lane, winw, wsA, wsB);
+        wave_lds_sync();
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        const uint64_t wb = a0 & ~127ull;
+        auto seg_store = [&](uint64_t d) {
+            const u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - wb));
+            if constexpr (NOSTORE) asm volatile("" ::"v"(x), "v"(d));
+            else *(GMEM u32x2*)d = x;
+        };
+        if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
+        if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
+    } else {
+        if (mine)
+            finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, lane == 0 ? tot : 0u, rd, winb, hd, a0,
+                                                                         r, lane);
+    }
+}
+
+// records per wavefront for a record length (0: not served)
+static int xwalk_records(uint32_t len) {
+    if (len < 1024) return 0;
+    for (int R = 8; R >= 1; R /= 2)
+        if (len <= 1024u * (16 / R) - 127u) return R;
+    return 0;
+}
+
+template <int R>
+static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams& p, hipStream_t s) {
+    const bool seg = variant % 64 == 47;
+    if (mode == MODE_VERIFY) {
+        hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+#ifdef SMOL_EXP
+    if (variant >= 64) {
+        if (seg) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, true, true>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, true, false>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+#endif
+    if (seg) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true>), dim3(blocks), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
+}
+
+bool xwalk_fits(const KParams& p) { return p.desc == nullptr && p.len == p.stride && xwalk_records(p.len) > 0; }
+
+hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s) {
+    const int R = xwalk_records(p.len);
+    const uint64_t per = (uint64_t)xwalk::WAVES * R;
+    const uint32_t b = grid_blocks((p.n + per - 1) / per, 0x7fffffff);
+    note_launch(KERN_XWALK, (uint32_t)variant, 64 / R, 16 / R);
+    switch (R) {
+        case 8: launch_xwalk_r<8>(mode, variant, b, p, s); break;
+        case 4: launch_xwalk_r<4>(mode, variant, b, p, s); break;
+        case 2: launch_xwalk_r<2>(mode, variant, b, p, s); break;
+        case 1: launch_xwalk_r<1>(mode, variant, b, p, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace smolcsum

@@ -672,18 +672,35 @@ def test_variants_fixed_stride(eng, variant):
                     assert np.array_equal(est.cpu().numpy(), ref_es)
 
 
-def test_stripe_kernel(eng):
-    """The stripe kernel (variant 42: packed fixed-stride records of 1024-1520 bytes, a wavefront
-    streams 8 records as wave-contiguous 1-KiB pieces) against the oracle: every profile, odd record
-    lengths (odd starts), batch sizes that leave a partial last wavefront, 1/7 corrupted, caps
-    variants; the whole buffer is compared after emit.  Batches it does not serve (gapped strides,
-    other lengths, descriptor batches) fall back to the walk kernel."""
-    eng.need(42)
-    for profile, kind, L in [(E.SYNTH_UDP4, E.KIND_IP, 1500), (E.SYNTH_UDP4, E.KIND_IP, 1024),
-                             (E.SYNTH_V6MIX, E.KIND_IP, 1320), (E.SYNTH_TCP4, E.KIND_IP, 1499),
-                             (E.SYNTH_ETH_TCP4, E.KIND_ETH, 1514), (E.SYNTH_TCP4, E.KIND_IP, 1025),
-                             (E.SYNTH_V6MIX, E.KIND_IP, 1519), (E.SYNTH_UDP4, E.KIND_IP, 1520)]:
-        for n, off in ((1, 0), (7, 3), (8, 0), (9, 64), (257, 1), (4099, 17)):
+WIDE_KERNELS = {
+    # variant: (kernel name, the largest record length it serves)
+    42: ("csum_tile_kernel", 1520),
+    44: ("xwalk_kernel", 16257),
+    47: ("xwalk_kernel", 16257),
+}
+
+
+@pytest.mark.parametrize("variant", sorted(WIDE_KERNELS))
+def test_wide_record_kernels(eng, variant):
+    """The experiment kernels for packed fixed-stride records of 1024 bytes and more (variant 42,
+    the stripe kernel: a wavefront streams 8 records as wave-contiguous 1-KiB pieces; variant 44, the
+    transposed walk: the same loads with the walk kernel's per-record parse and finish, 8 / 4 / 2 / 1
+    records per wavefront up to 1921 / 3969 / 8065 / 16257 B; 47: 44 with whole field segments) against the
+    oracle: every profile, odd record lengths (odd starts), batch sizes that leave a partial last
+    wavefront, 1/7 corrupted, caps variants; the whole buffer is compared after emit.  Batches they
+    do not serve (gapped strides, other lengths, descriptor batches) fall back to the walk kernel."""
+    eng.need(variant)
+    kname, lmax = WIDE_KERNELS[variant]
+    lens = [(E.SYNTH_UDP4, E.KIND_IP, 1500), (E.SYNTH_UDP4, E.KIND_IP, 1024),
+            (E.SYNTH_V6MIX, E.KIND_IP, 1320), (E.SYNTH_TCP4, E.KIND_IP, 1499),
+            (E.SYNTH_ETH_TCP4, E.KIND_ETH, 1514), (E.SYNTH_TCP4, E.KIND_IP, 1025),
+            (E.SYNTH_V6MIX, E.KIND_IP, 1519), (E.SYNTH_UDP4, E.KIND_IP, 1520)]
+    if lmax > 1520:  # every records-per-wavefront form, at both ends of its range
+        lens += [(E.SYNTH_V6MIX, E.KIND_IP, 1777), (E.SYNTH_TCP4, E.KIND_IP, 1921), (E.SYNTH_UDP4, E.KIND_IP, 1922),
+                 (E.SYNTH_V6MIX, E.KIND_IP, 3001), (E.SYNTH_TCP4, E.KIND_IP, 3969), (E.SYNTH_ETH_TCP4, E.KIND_ETH, 3970),
+                 (E.SYNTH_UDP4, E.KIND_IP, 8065), (E.SYNTH_V6MIX, E.KIND_IP, 8066), (E.SYNTH_TCP4, E.KIND_IP, lmax)]
+    for profile, kind, L in lens:
+        for n, off in ((1, 0), (7, 3), (8, 0), (9, 64), (257, 1), (4099 if L < 4000 else 1029, 17)):
             host = np.zeros(off + n * L + 128, dtype=np.uint8)
             tmp = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
             batch = E.Batch.fixed(n, L, L, kind)
@@ -692,38 +709,89 @@ def test_stripe_kernel(eng):
             eng.corrupt(tmp, batch, every=7, seed=n)
             host[off:off + tmp.numel()] = tmp.cpu().numpy()
             for caps in (CAPS_DEFAULT, (2, 3, 0, 1, 0)):
-                d = torch.from_numpy(host.copy()).cuda()
-                view = d[off:]
-                eng.set_variant(42)
-                try:
-                    st = eng.verify(view, batch, caps=caps).cpu().numpy()
-                    lv = eng.last_launch()
-                    eng.emit(view, batch, caps=caps)
-                    le = eng.last_launch()
-                finally:
-                    eng.set_variant(-1)
-                assert (lv["kernel"], lv["variant"]) == ("csum_tile_kernel", 42), lv
-                assert (le["kernel"], le["variant"]) == ("csum_tile_kernel", 42), le
-                ref_v = oracle.batch_verify(host[off:].copy(), None, n, L, L, kind, caps)
-                assert np.array_equal(st, ref_v), (L, n, off, caps, np.nonzero(st != ref_v)[0][:8])
-                ref_e = host.copy()
-                oracle.batch_emit(ref_e[off:], None, n, L, L, kind, caps)
-                got = d.cpu().numpy()
-                assert np.array_equal(got, ref_e), (L, n, off, caps, np.nonzero(got != ref_e)[0][:8])
-    # not served: gapped stride, a length outside 1024-1520 -> the walk kernel
-    for L, stride in ((1500, 1501), (1000, 1000), (1600, 1600)):
+                _wide_case(eng, variant, kname, host, off, n, L, kind, caps)
+    # not served: gapped stride, a length outside the kernel's range -> the walk kernel
+    for L, stride in ((1500, 1501), (1000, 1000), (lmax + 1, lmax + 1)):
         n = 100
         buf = torch.zeros(n * stride + 64, dtype=torch.uint8, device="cuda:0")
         batch = E.Batch.fixed(n, stride, L, E.KIND_IP)
         eng.synth(buf, batch, E.SYNTH_UDP4, seed=L)
         host = buf.cpu().numpy().copy()
-        eng.set_variant(42)
+        eng.set_variant(variant)
         try:
             st = eng.verify(buf, batch).cpu().numpy()
             assert eng.last_launch()["kernel"] == "csum_kernel"
         finally:
             eng.set_variant(-1)
         assert np.array_equal(st, oracle.batch_verify(host, None, n, stride, L, E.KIND_IP, CAPS_DEFAULT))
+
+
+def _wide_case(eng, variant, kname, host, off, n, L, kind, caps):
+    batch = E.Batch.fixed(n, L, L, kind)
+    d = torch.from_numpy(host.copy()).cuda()
+    view = d[off:]
+    eng.set_variant(variant)
+    try:
+        st = eng.verify(view, batch, caps=caps).cpu().numpy()
+        lv = eng.last_launch()
+        eng.emit(view, batch, caps=caps)
+        le = eng.last_launch()
+    finally:
+        eng.set_variant(-1)
+    assert (lv["kernel"], lv["variant"]) == (kname, variant), lv
+    assert (le["kernel"], le["variant"]) == (kname, variant), le
+    ref_v = oracle.batch_verify(host[off:].copy(), None, n, L, L, kind, caps)
+    assert np.array_equal(st, ref_v), (L, n, off, caps, np.nonzero(st != ref_v)[0][:8])
+    ref_e = host.copy()
+    oracle.batch_emit(ref_e[off:], None, n, L, L, kind, caps)
+    got = d.cpu().numpy()
+    assert np.array_equal(got, ref_e), (L, n, off, caps, np.nonzero(got != ref_e)[0][:8])
+
+
+@pytest.mark.parametrize("variant", sorted(WIDE_KERNELS))
+def test_wide_record_kernels_edge_records(eng, variant):
+    """The same kernels on records whose checksummed span ends before the record's end (IP total
+    length / UDP length below the slot, random trailing bytes), truncated and garbage headers, IPv6
+    Hop-by-Hop options past the LDS window, zero-length payloads: slots of 1024 .. the largest
+    length, packed, verify after emit and after corruption, against the oracle."""
+    eng.need(variant)
+    kname, lmax = WIDE_KERNELS[variant]
+    rng = np.random.default_rng(43 + variant)
+    for L in sorted({1024, 1100, 1337, 1500, min(lmax, 1921), min(lmax, 2600), min(lmax, 5000), lmax}):
+        recs = []
+        for i in range(300):
+            pl = P.rand_bytes(rng, int(rng.integers(0, L - 120)))
+            m = i % 8
+            if m == 0:
+                r = P.ipv4(V4A, V4B, 17, P.udp(1, 2, pl))
+            elif m == 1:
+                r = P.ipv4(V4A, V4B, 6, P.tcp(1, 2, pl))
+            elif m == 2:
+                r = P.ipv6(P.rand_bytes(rng, 16), P.rand_bytes(rng, 16), 58, P.icmp_echo(128, pl))
+            elif m == 3:
+                opts = bytes([1, 250]) + bytes(250) + P.random_hbh_options(rng)
+                r = P.ipv6(P.rand_bytes(rng, 16), P.rand_bytes(rng, 16), 0, P.hbh_opts(17, opts) + P.udp(3, 4, pl[:400]))
+            elif m == 4:
+                u = bytearray(P.udp(1, 2, pl))
+                ul = int(rng.integers(8, len(u) + 1))  # UDP length below the IP payload
+                u[4:6] = ul.to_bytes(2, "big")
+                r = P.ipv4(V4A, V4B, 17, bytes(u))
+            elif m == 5:
+                r = P.ipv4(V4A, V4B, 17, P.udp(1, 2, b""))
+            elif m == 6:
+                r = P.rand_bytes(rng, int(rng.integers(0, L + 1)))
+            else:
+                r = P.ipv6(bytes(16), bytes(16), 6, P.tcp(1, 2, pl))[: int(rng.integers(0, 80))]
+            r = r[:L]
+            recs.append(r + P.rand_bytes(rng, L - len(r)))
+        host = np.frombuffer(b"".join(recs) + bytes(128), dtype=np.uint8).copy()
+        n = len(recs)
+        P.oracle_emit_records(host, np.arange(n) * L, np.full(n, L), np.full(n, E.KIND_IP, np.uint8), CAPS_DEFAULT)
+        for k in range(0, n, 5):  # every fifth record: one byte inside its first 1 KiB flipped
+            host[k * L + int(rng.integers(0, 1024))] ^= 0x5A
+        for off in (0, 1):
+            h = np.concatenate([np.zeros(off, np.uint8), host])
+            _wide_case(eng, variant, kname, h, off, n, L, E.KIND_IP, CAPS_DEFAULT)
 
 
 def test_pretty_print_annotations(eng, golden):

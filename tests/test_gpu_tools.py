@@ -51,7 +51,19 @@ def test_last_launch_families(eng):
     assert (ll["kernel"], ll["variant"], ll["G"]) == ("csum_kernel", 39, 8), ll
     eng.verify(buf, b)
     ll = eng.last_launch()
-    assert (ll["kernel"], ll["variant"]) == ("csum_kernel", 5), ll
+    # packed fixed-stride verify of 1473 .. 8065-B records: the transposed walk, 8 records per wavefront
+    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("xwalk_kernel", 47, 8, 2), ll
+    X, W = "xwalk_kernel", "csum_kernel"
+    for LL, stride, op, want in ((1320, 1320, "verify", (W, 5, 8)), (1500, 1501, "verify", (W, 5, 8)),
+                                 (2500, 2500, "emit", (X, 47, 16)), (2500, 2500, "verify", (X, 47, 16)),
+                                 (1500, 1500, "emit", (W, 39, 8)), (9000, 9000, "verify", (W, 5, None)),
+                                 (9000, 9000, "emit", (X, 47, 64)), (12000, 12000, "emit", (W, 39, None))):
+        bb = E.Batch.fixed(8, stride, LL, E.KIND_IP)
+        t = torch.zeros(8 * stride + 64, dtype=torch.uint8, device="cuda:0")
+        getattr(eng, op)(t, bb)
+        ll = eng.last_launch()
+        assert (ll["kernel"], ll["variant"]) == want[:2], (LL, stride, op, ll)
+        assert want[2] is None or ll["G"] == want[2], (LL, stride, op, ll)
     offs = np.arange(n, dtype=np.uint64) * L
     bd = E.Batch.from_records(offs, np.full(n, L, np.uint32), E.KIND_IP, "cuda:0")
     eng.emit(buf, bd)

@@ -4,7 +4,9 @@ batches in turn (every emit a batch its previous pass did not just write, as the
 do since round 5), interleaved rounds on one box.  Verify of the RX batch is timed in the same
 rounds as the reference.  Store variants must leave the bytes of the first variant listed; `| 64`
 variants (experiments: stores compiled out) are timing only.
-Usage: [VARS=29,5,31,32] [VVARS=-1,13 (verify variants)] [K=32] [ROUNDS=4] exp_r05_emit.py [c2,c4]"""
+XCDS=-1,1,16: the emit variants under each XCD block mapping in turn (smol_csum_set_xcd_remap; -1 the
+default), reported as `<variant>x<remap>`.
+Usage: [VARS=29,5,31,32] [VVARS=-1,13 (verify variants)] [XCDS=-1] [K=32] [ROUNDS=4] exp_r05_emit.py [c2,c4]"""
 import json
 import os
 import sys
@@ -74,12 +76,15 @@ def main():
                 ver = timed(lambda j: eng.verify(wl.rxs[j], wl.batch, status=wl.status))
                 name = "verify" if vv < 0 else f"verify{vv}"
                 print(json.dumps({"round": rnd, "cfg": c, "variant": name, "ms": round(ver, 4)}), flush=True)
-            for v in vars_:
-                eng.set_variant(v)
-                fresh = timed(lambda j: eng.emit(wl.txs[j], wl.batch))
-                same = timed(lambda j: eng.emit(wl.txs[0], wl.batch))
-                print(json.dumps({"round": rnd, "cfg": c, "variant": v, "emit_fresh_ms": round(fresh, 4),
-                                  "emit_same_ms": round(same, 4)}), flush=True)
+            for x in [int(y) for y in os.environ.get("XCDS", "-1").split(",")]:
+                eng.set_xcd_remap(x)
+                for v in vars_:
+                    eng.set_variant(v)
+                    fresh = timed(lambda j: eng.emit(wl.txs[j], wl.batch))
+                    same = timed(lambda j: eng.emit(wl.txs[0], wl.batch))
+                    print(json.dumps({"round": rnd, "cfg": c, "variant": v if x < 0 else f"{v}x{x}",
+                                      "emit_fresh_ms": round(fresh, 4), "emit_same_ms": round(same, 4)}), flush=True)
+                eng.set_xcd_remap(-1)
     eng.set_variant(-1)
 
 
