@@ -103,19 +103,20 @@ int walk_variant(int mode, bool has_desc) {
 }
 int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
 
-// Round 5: the transposed walk (csum_xwalk.hip, variant 47: emit with whole field segments) for packed
-// fixed-stride records where it beats the walk kernel.  Verify and emit of synthetic IPv4/UDP over
+// Round 5: the transposed walk (csum_xwalk.hip, variant 47: emit with whole field segments) for
+// fixed-stride records where it beats the walk kernel.  Verify / emit of synthetic IPv4/UDP over
 // ~1.5 GB, R = 4 batches in turn, one box (tools/exp_r05_vlen.py, profiles/r05_experiments/
-// xwalk_lengths.jsonl), walk -> transposed walk in TB/s: verify 1500 B 6.41 -> 6.65, 1760 B 4.34 ->
-// 6.98, 2500 B 2.89 -> 6.45, 3969 B 4.43 -> 6.73, 5000 B 4.65 -> 6.42, 8065 B 6.51 -> 6.65, and
-// slower at 1024 / 1320 B (6.13 / 6.67 -> 5.29 / 6.33) and from 9000 B (6.44 -> 6.27); emit
-// 1500 B 4.99 -> 4.77 (slower), 1760 B 3.35 -> 5.41, 2500 B 2.59 -> 5.36, 9000 B 5.66 -> 6.22,
-// 12000 B 6.18 -> 6.07.
+// xwalk_vs_walk_packed.jsonl, xwalk_vs_walk_gap64.jsonl), walk / transposed walk time, packed:
+//   length   1024 1320 1472 1500 1600 1700 1921 2500 3969 5000 8065 9000 12000 16257
+//   verify   0.89 0.96 1.00 1.05 0.99 1.78 1.55 2.27 1.51 1.50 1.04 1.05  0.99  0.98
+//   emit     1.01 0.96 0.97 0.94 0.96 1.68 1.53 2.10 1.44 1.39 1.01 1.08  1.00  1.00
+// and with 64-B gaps verify 0.91 (1024) 0.92 (1320) 1.00 (1500) 1.72 (1700) 2.22 (2500) 1.49 (5000)
+// 1.06 (9000) 1.00 (12000), emit within 2 % of that.  The walk kernel's shapes leave lanes idle from
+// 1666 B (8 x 7 x 2 chunks no longer hold a record); 1500 B packed is a weak spot of its line grid.
 bool xwalk_auto(int mode, const smol_csum_batch_t* b) {
-    if (b->desc || b->stride != b->len) return false;
-    if (mode == MODE_VERIFY) return b->len >= 1473 && b->len <= 8065;
-    if (mode == MODE_EMIT) return b->len >= 1666 && b->len <= 10000;
-    return false;
+    if (b->desc || b->stride < b->len) return false;
+    const uint32_t lo = (mode == MODE_VERIFY && b->stride == b->len) ? 1473u : 1666u;
+    return (mode == MODE_VERIFY || mode == MODE_EMIT) && b->len >= lo && b->len <= 10000;
 }
 
 // The XCD block order (csum_launch.h xcd_block / xcd_chunk) when none is forced: the contiguous order
@@ -235,7 +236,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     // the stripe kernel (variant 42) serves emit / verify of packed fixed-stride records of 1024-1520 B
     const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
     if (variant == 42 && !stripe) variant = walk_variant(mode, has_desc);
-    // the transposed walk (variants 44 / 47, 64 + 44 / 47): packed records of 1024 - 16257 B
+    // the transposed walk (variants 44 / 47, 64 + 44 / 47): fixed-stride records of 1024 - 16257 B
     const bool xw_var = variant % 64 == 44 || variant % 64 == 47;
     const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
     if (xw_var && !xwalk) variant = walk_variant(mode, has_desc);

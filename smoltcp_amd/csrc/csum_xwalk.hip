@@ -1,5 +1,5 @@
-// Transposed walk (variants 44 / 47): fixed-stride emit / verify of packed
-// records of 1024 .. 16257 bytes over a natural grid, with the walk kernel's per-record work (a group
+// Transposed walk (variants 44 / 47): fixed-stride emit / verify of records of 1024 .. 16257 bytes
+// (packed or with gaps) over a natural grid, with the walk kernel's per-record work (a group
 // of G lanes parses and finishes one record, R = 64 / G records per wavefront) and a different load
 // mapping.
 //
@@ -16,15 +16,12 @@
 //
 // Sums.  A lane adds its chunk of record j to its accumulator j (j is a compile-time index), and a
 // reduce-scatter over the wavefront (exchanges across 32, 16, .., G lanes, then the group's own
-// reduction) leaves record j's sum in group j.  Chunks are summed whole where that is exact and
-// corrected in the finish from the LDS windows:
+// reduction) leaves record j's sum in group j.  Chunks are summed whole, up to the one holding the
+// span's end (whose bytes past it its lane takes out again), and corrected from the LDS windows:
 //  - the bytes of a record's first line before its start belong to the previous record:
-//    subtracted (hs_j, from record j's window) and, when the previous record is in this wavefront,
-//    added to that record, which does not load the line (the line holding record j + 1's first
-//    byte is loaded once, as record j + 1's first chunk: csum_walk.h shared_from);
-//  - a record whose checksummed span ends before its end (UDP length < the IP payload, malformed or
-//    unsupported records), and the wavefront's last record (its last line is the next wavefront's),
-//    mask every chunk to [0, span_end) instead (the walk's masked sum).
+//    subtracted (hs_j, from record j's window) and, for packed records whose previous record is in
+//    this wavefront, added to that record, which does not load the line (the line holding record
+//    j + 1's first byte is loaded once, as record j + 1's first chunk: csum_walk.h shared_from).
 //
 // Measured (profiles/r05_experiments/xwalk_*.txt): the other forms tried, a 64-bit-address load from
 // the dummy line for out-of-range chunks, a persistent grid (one wavefront steps over the batch 8
@@ -37,13 +34,6 @@ namespace xwalk {
 
 constexpr int WIN_CH = 16;  // the LDS window: 256 B from the record's 128-B line
 constexpr int WAVES = 4;    // wavefronts per workgroup
-
-// Sum of the words of `c` with record offsets in [0, hi) (pos: the chunk's first byte, relative to
-// the record start).
-__device__ __forceinline__ uint32_t span_sum(const u32x4& c, int pos, int hi) {
-    if (pos >= 0 && pos + 16 <= hi) return add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u))));
-    return sum_masked_words(c, -pos, hi - pos, 0u);
-}
 
 // The value of lane ^ H (H = 32 / 16 / 8 / ..: across the wavefront, a 32-lane half, a row)
 template <int H>
@@ -97,6 +87,9 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     const uint32_t cnt = (uint32_t)(p.n - rw0 < (uint64_t)R ? p.n - rw0 : (uint64_t)R);
     const uint32_t len = p.len;
     const uint64_t stride = p.stride;
+    // packed records share lines with their neighbours (each line is loaded once); with a gap every
+    // record loads all its lines and sums them masked to its span
+    const bool packed = stride == (uint64_t)len;
 
     // ---- all loads of the wavefront's records (record j: chunks below nload_j of its line grid) ----
     u32x4 v[NS][R];
@@ -112,8 +105,8 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
         const uint64_t b = a0 & ~127ull;
         head[j] = (uint32_t)(a0 - b);
         const uint32_t nch = (uint32_t)j < cnt ? (uint32_t)(((a0 + len + 15) >> 4) - (b >> 4)) : 0u;
-        // the line holding record j + 1's first byte is record j + 1's to load
-        const bool shared = (uint32_t)j + 1 < cnt;
+        // packed: the line holding record j + 1's first byte is record j + 1's to load
+        const bool shared = packed && (uint32_t)j + 1 < cnt;
         nload[j] = shared ? (uint32_t)((((a0 + stride) & ~127ull) - b) >> 4) : nch;
         const int soff = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b - wbase));
 #pragma unroll
@@ -156,41 +149,42 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     for (int j = 0; j < R; ++j) span[j] = (int)spanbuf[wv * R + j];
 
     // ---- sums: accumulator j of every lane holds its chunks of record j ----
+    // Chunks below kend_j (the loaded chunks up to the span's end) are summed whole; the lane whose
+    // chunk holds the span's end takes the bytes past it out again.  The bytes before the record in
+    // its first line (hs) come out after the reduction.
     uint32_t acc[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         acc[j] = 0;
-        // whole chunks: the span runs to the record's end and the next record takes the last line
-        const bool whole = (uint32_t)j + 1 < cnt && span[j] == (int)len;
+        const int hj = (int)head[j], sj = span[j];
+        const uint32_t kend = min(nload[j], (uint32_t)(hj + sj + 15) >> 4);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const uint32_t k = (uint32_t)(64 * s + wl);
             const u32x4 c = v[s][j];
-            uint32_t x;
-            if (whole) x = add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u))));
-            else x = span_sum(c, 16 * (int)k - (int)head[j], span[j]);
-            acc[j] += k < nload[j] ? x : 0u;
+            const int pos = 16 * (int)k - hj;
+            uint32_t x = k < kend ? add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u)))) : 0u;
+            if (k < kend && pos + 16 > sj) x -= sum_masked_words(c, sj - pos, 16, 0u);
+            acc[j] += x;
         }
     }
     // ---- reduce-scatter: record j's sum to group j ----
-    uint32_t tot = group_sum<G>(reduce_scatter<R, 32>(acc, wl));
-    // corrections: the first line's bytes before the record (whole-chunk records only), and the
-    // last line's bytes of this record that record j + 1 loaded (its hs)
+    uint32_t tot = group_sum<G>(reduce_scatter<R, 32>(acc, wl)) - hs;
+    // packed: the bytes of this record's last line, which record j + 1 loaded, are record offsets
+    // [len - hdn, len) = record j + 1's window bytes [0, hdn) (its hs when the span runs to the end)
     const uint32_t hs_next = (uint32_t)__shfl_down((int)hs, G, 64);
-    const bool whole = (uint32_t)gw + 1 < cnt && s1 == (int)len;
-    if (whole) {
-        tot = tot - hs + hs_next;
-    } else if ((uint32_t)gw + 1 < cnt) {
-        // masked sums: the first line's extra bytes were masked out; the bytes record j + 1 loaded
-        // are record offsets [len - hdn, len) = its window's bytes [0, hdn), counted below the
-        // span's end
-        const uint32_t hdn = (uint32_t)((a0 + stride) & 127u);
-        const int lim = min((int)hdn, s1 - ((int)len - (int)hdn));
-        uint32_t t = 0;
+    if (packed && (uint32_t)gw + 1 < cnt) {
+        if (s1 == (int)len) {
+            tot += hs_next;
+        } else {
+            const uint32_t hdn = (uint32_t)((a0 + stride) & 127u);
+            const int lim = min((int)hdn, s1 - ((int)len - (int)hdn));
+            uint32_t t = 0;
 #pragma unroll
-        for (int c = 0; c < WIN_CH; c += G)
-            if (c + lane < WIN_CH) t = sum_masked_words(win[gib + 1][c + lane], 0, lim - 16 * (c + lane), t);
-        tot += group_sum<G>(t);
+            for (int c = 0; c < WIN_CH; c += G)
+                if (c + lane < WIN_CH) t = sum_masked_words(win[gib + 1][c + lane], 0, lim - 16 * (c + lane), t);
+            tot += group_sum<G>(t);
+        }
     }
     // ---- finish: the walk kernel's gates (lane 0 writes) ----
     if constexpr (EMIT && SEG) {
@@ -265,7 +259,10 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
     else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
 }
 
-bool xwalk_fits(const KParams& p) { return p.desc == nullptr && p.len == p.stride && xwalk_records(p.len) > 0; }
+bool xwalk_fits(const KParams& p) {
+    // the buffer offsets of a wavefront's records stay below 2^31
+    return p.desc == nullptr && p.stride >= p.len && p.stride <= (1ull << 26) && xwalk_records(p.len) > 0;
+}
 
 hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s) {
     const int R = xwalk_records(p.len);

@@ -710,8 +710,26 @@ def test_wide_record_kernels(eng, variant):
             host[off:off + tmp.numel()] = tmp.cpu().numpy()
             for caps in (CAPS_DEFAULT, (2, 3, 0, 1, 0)):
                 _wide_case(eng, variant, kname, host, off, n, L, kind, caps)
-    # not served: gapped stride, a length outside the kernel's range -> the walk kernel
-    for L, stride in ((1500, 1501), (1000, 1000), (lmax + 1, lmax + 1)):
+    if kname == "xwalk_kernel":  # gapped strides, random bytes in the gaps
+        rng = np.random.default_rng(variant)
+        for profile, L in ((E.SYNTH_UDP4, 1024), (E.SYNTH_UDP4, 1500), (E.SYNTH_V6MIX, 2500), (E.SYNTH_TCP4, 5000),
+                           (E.SYNTH_V6MIX, 9000)):
+            for gap in (1, 63, 200):
+                stride = L + gap
+                for n, off in ((9, 1), (1029, 0)):
+                    tmp = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+                    pb = E.Batch.fixed(n, L, L, E.KIND_IP)
+                    eng.synth(tmp, pb, profile, seed=L + gap + n)
+                    eng.emit(tmp, pb)
+                    eng.corrupt(tmp, pb, every=7, seed=n)
+                    recs = tmp.cpu().numpy()[: n * L].reshape(n, L)
+                    host = rng.integers(0, 256, off + n * stride + 128, dtype=np.uint8)
+                    for i in range(n):
+                        host[off + i * stride: off + i * stride + L] = recs[i]
+                    _wide_case(eng, variant, kname, host, off, n, L, E.KIND_IP, CAPS_DEFAULT, stride)
+    # not served: a length outside the kernel's range -> the walk kernel
+    stripe_gap = ((1500, 1501),) if kname != "xwalk_kernel" else ()
+    for L, stride in stripe_gap + ((1000, 1000), (lmax + 1, lmax + 1)):
         n = 100
         buf = torch.zeros(n * stride + 64, dtype=torch.uint8, device="cuda:0")
         batch = E.Batch.fixed(n, stride, L, E.KIND_IP)
@@ -726,8 +744,9 @@ def test_wide_record_kernels(eng, variant):
         assert np.array_equal(st, oracle.batch_verify(host, None, n, stride, L, E.KIND_IP, CAPS_DEFAULT))
 
 
-def _wide_case(eng, variant, kname, host, off, n, L, kind, caps):
-    batch = E.Batch.fixed(n, L, L, kind)
+def _wide_case(eng, variant, kname, host, off, n, L, kind, caps, stride=None):
+    stride = stride or L
+    batch = E.Batch.fixed(n, stride, L, kind)
     d = torch.from_numpy(host.copy()).cuda()
     view = d[off:]
     eng.set_variant(variant)
@@ -740,12 +759,12 @@ def _wide_case(eng, variant, kname, host, off, n, L, kind, caps):
         eng.set_variant(-1)
     assert (lv["kernel"], lv["variant"]) == (kname, variant), lv
     assert (le["kernel"], le["variant"]) == (kname, variant), le
-    ref_v = oracle.batch_verify(host[off:].copy(), None, n, L, L, kind, caps)
-    assert np.array_equal(st, ref_v), (L, n, off, caps, np.nonzero(st != ref_v)[0][:8])
+    ref_v = oracle.batch_verify(host[off:].copy(), None, n, stride, L, kind, caps)
+    assert np.array_equal(st, ref_v), (L, stride, n, off, caps, np.nonzero(st != ref_v)[0][:8])
     ref_e = host.copy()
-    oracle.batch_emit(ref_e[off:], None, n, L, L, kind, caps)
+    oracle.batch_emit(ref_e[off:], None, n, stride, L, kind, caps)
     got = d.cpu().numpy()
-    assert np.array_equal(got, ref_e), (L, n, off, caps, np.nonzero(got != ref_e)[0][:8])
+    assert np.array_equal(got, ref_e), (L, stride, n, off, caps, np.nonzero(got != ref_e)[0][:8])
 
 
 @pytest.mark.parametrize("variant", sorted(WIDE_KERNELS))

@@ -3,7 +3,8 @@
 transposed walk (variants 44 / 47) over record lengths, ~1.5 GB per batch, R = 4 batches in turn
 (synthetic IPv4/UDP, every 64th record corrupted; emit timed after verify on the same batches).
 Needs the experiments build (SMOLCSUM_LIB=.../libsmolcsum_exp.so).
-Usage: [LENS=1024,1320,1500] [VVARS=-1,44] [EVARS=-1,44,47] [K=24] exp_r05_vlen.py"""
+GAP=g: stride = length + g (default 0, packed).
+Usage: [LENS=1024,1320,1500] [VVARS=-1,44] [EVARS=-1,44,47] [GAP=0] [K=24] exp_r05_vlen.py"""
 import json
 import os
 import sys
@@ -23,11 +24,12 @@ def main():
     vv = [int(x) for x in os.environ.get("VVARS", "-1,44").split(",")]
     ev = [int(x) for x in os.environ.get("EVARS", "-1,44,47").split(",") if x]
     for L in lens:
-        n = (1536 << 20) // L
-        batch = E.Batch.fixed(n, L, L, E.KIND_IP)
+        S = L + int(os.environ.get("GAP", "0"))
+        n = (1536 << 20) // S
+        batch = E.Batch.fixed(n, S, L, E.KIND_IP)
         rxs = []
         for j in range(R):
-            b = torch.empty(n * L + 64, dtype=torch.uint8, device="cuda:0")
+            b = torch.empty(n * S + 64, dtype=torch.uint8, device="cuda:0")
             eng.synth(b, batch, E.SYNTH_UDP4, seed=L + j)
             eng.emit(b, batch)
             eng.corrupt(b, batch, every=64, seed=j)
@@ -59,7 +61,7 @@ def main():
                 eng.set_variant(v)
                 res.setdefault(f"emit{v}", []).append(timed(lambda j: eng.emit(rxs[j], batch)))
         eng.set_variant(-1)
-        print(json.dumps({"len": L, "n": n, **{k: round(min(t), 4) for k, t in res.items()},
+        print(json.dumps({"len": L, "stride": S, "n": n, **{k: round(min(t), 4) for k, t in res.items()},
                           **{f"TBps_{k}": round(n * L / min(t) / 1e9, 2) for k, t in res.items()}}), flush=True)
         del rxs
 
