@@ -266,17 +266,28 @@ bool xwalk_fits(const KParams& p) {
 
 hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s) {
     const int R = xwalk_records(p.len);
+    if (R == 0) return hipErrorInvalidValue;
     const uint64_t per = (uint64_t)xwalk::WAVES * R;
-    const uint32_t b = grid_blocks((p.n + per - 1) / per, 0x7fffffff);
     note_launch(KERN_XWALK, (uint32_t)variant, 64 / R, 16 / R);
-    switch (R) {
-        case 8: launch_xwalk_r<8>(mode, variant, b, p, s); break;
-        case 4: launch_xwalk_r<4>(mode, variant, b, p, s); break;
-        case 2: launch_xwalk_r<2>(mode, variant, b, p, s); break;
-        case 1: launch_xwalk_r<1>(mode, variant, b, p, s); break;
-        default: return hipErrorInvalidValue;
+    // one workgroup per 4R records and no grid-stride loop: a batch past kMaxGridBlocks workgroups
+    // (more records than 288 GB of HBM holds at these lengths) goes out as several launches
+    const uint64_t span = kMaxGridBlocks * per;
+    for (uint64_t i0 = 0; i0 < p.n; i0 += span) {
+        KParams q = p;
+        q.n = p.n - i0 < span ? p.n - i0 : span;
+        q.buf = p.buf + i0 * p.stride;
+        if (p.status) q.status = p.status + i0;
+        const uint32_t b = grid_blocks((q.n + per - 1) / per, kMaxGridBlocks);
+        switch (R) {
+            case 8: launch_xwalk_r<8>(mode, variant, b, q, s); break;
+            case 4: launch_xwalk_r<4>(mode, variant, b, q, s); break;
+            case 2: launch_xwalk_r<2>(mode, variant, b, q, s); break;
+            default: launch_xwalk_r<1>(mode, variant, b, q, s); break;
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 }  // namespace smolcsum
