@@ -189,8 +189,8 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     // ---- finish: the walk kernel's gates (lane 0 writes) ----
     if constexpr (EMIT && SEG) {
         // A segment that starts before the record also holds record r-1's last bytes: whole only
-        // when r-1 has no field in its last 64 bytes (its group says so: ok_tail) and r-1 is in this
-        // wavefront.  A record whose fields end 64 bytes or more before its end never reaches into
+        // for packed records, when r-1 has no field in its last 64 bytes (its group says so:
+        // ok_tail) and r-1 is in this wavefront.  A record whose fields end 64 bytes or more before its end never reaches into
         // r+1 with its own segments.
         uint32_t f[3], lo = NO_FIELD, hi = 0;
         emit_fields(g, f);
@@ -204,7 +204,8 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
         const uint64_t okm = __ballot(lane == 0 && mine && ok_tail);
         uint64_t wsA = ~0ull, wsB = ~0ull;
         if (mine && (g.fam == 4 || g.fam == 6) && hi != 0 && ok_tail) {
-            const bool prev_ok = gw != 0 && ((okm >> (wl - lane - G)) & 1ull);
+            // gapped strides: the record's own bytes only (a gap is never written)
+            const bool prev_ok = packed && gw != 0 && ((okm >> (wl - lane - G)) & 1ull);
             const int32_t ph = (int32_t)(a0 & 63u);
             const int32_t rA = ((ph + (int32_t)lo) & ~63) - ph, rB = ((ph + (int32_t)hi - 1) & ~63) - ph;
             const int32_t wend = 16 * WIN_CH - (int32_t)hd;

@@ -206,13 +206,14 @@ def test_c3_seed_segments(eng):
     _desc_case(eng, buf.cpu().numpy().copy(), offs, lens, E.KIND_IP, blocks_list=(0, 5))
 
 
-@pytest.mark.parametrize("gap", [0, 24])
-def test_emit_write_set_concurrent(eng, gap):
+@pytest.mark.parametrize("gap,L", [(0, 1500), (24, 1500), (0, 2500), (24, 2500), (40, 9000)])
+def test_emit_write_set_concurrent(eng, gap, L):
     """Emit never writes a byte outside its records: while emit runs on one stream, another stream
     rewrites every byte outside the records (before the batch, the gaps between records, after the
     batch) with 1, 2, ..., K.  Afterwards those bytes must all hold K and the records must equal the
-    oracle's emit.  Fixed-stride (variant 19 and the defaults) and descriptor batches."""
-    n, L = 1 << 15, 1500
+    oracle's emit.  Fixed-stride (variant 19, the transposed walk 44 / 47 and the defaults: 2500 B
+    and 9000 B run the transposed walk) and descriptor batches."""
+    n = (1 << 15) if L < 5000 else (1 << 12)
     stride = L + gap
     pre, post = 4096, 4096
     total = pre + n * stride + post
@@ -231,7 +232,7 @@ def test_emit_write_set_concurrent(eng, gap):
     s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
     K = 120
     for variant, batch in ((19, fixed), (29, fixed), (-1, fixed), (23, fixed), (26, desc_batch), (28, desc_batch),
-                           (-1, desc_batch), (37, fixed), (39, fixed)):
+                           (-1, desc_batch), (37, fixed), (39, fixed), (44, fixed), (47, fixed)):
         if not eng.has(variant):
             continue
         d = torch.from_numpy(host0.copy()).cuda()
@@ -275,20 +276,22 @@ def test_field_stores_flag(eng):
         finally:
             eng.set_variant(-1)
         assert np.array_equal(got, ref), (variant, np.nonzero(got != ref)[0][:8])
-    # a fixed-stride C2-like batch: UDP payload bytes 30..63 of every record (in the segment that
-    # holds the IPv4 header and UDP checksums) rewritten from another stream while emit runs
-    n, L = 1 << 15, 1500
-    buf = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
-    fixed = E.Batch.fixed(n, L, L, E.KIND_IP, flags=E.BATCH_FIELD_STORES)
-    eng.synth(buf, fixed, E.SYNTH_UDP4, seed=5)
-    payload = buf[: n * L].view(n, L)[:, 30:64]
-    s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
-    torch.cuda.synchronize()
-    K = 120
-    for k in range(1, K + 1):
-        with torch.cuda.stream(s_write):
-            payload.fill_(k)
-        if k % 12 == 1:
-            eng.emit(buf, fixed, stream=s_emit)
-    torch.cuda.synchronize()
-    assert bool((payload == K).all())
+    # fixed-stride C2-like batches (1500 B: the walk kernel; 2500 B: the transposed walk): UDP
+    # payload bytes 30..63 of every record (in the segment that holds the IPv4 header and UDP
+    # checksums) rewritten from another stream while emit runs
+    for n, L in ((1 << 15, 1500), (1 << 14, 2500)):
+        buf = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+        fixed = E.Batch.fixed(n, L, L, E.KIND_IP, flags=E.BATCH_FIELD_STORES)
+        eng.synth(buf, fixed, E.SYNTH_UDP4, seed=5)
+        payload = buf[: n * L].view(n, L)[:, 30:64]
+        s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
+        torch.cuda.synchronize()
+        K = 120
+        for k in range(1, K + 1):
+            with torch.cuda.stream(s_write):
+                payload.fill_(k)
+            if k % 12 == 1:
+                eng.emit(buf, fixed, stream=s_emit)
+        torch.cuda.synchronize()
+        assert bool((payload == K).all()), L
+        assert eng.last_launch()["kernel"] == ("xwalk_kernel" if L == 2500 else "csum_kernel")
