@@ -156,7 +156,7 @@ bool variant_built(int v) {
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 42;
+           (v >= 31 && v <= 38) || v == 42 || v == 48 || (v >= 49 && v <= 54);
 #else
     return false;
 #endif
@@ -237,7 +237,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
     if (variant == 42 && !stripe) variant = walk_variant(mode, has_desc);
     // the transposed walk (variants 44 / 47, 64 + 44 / 47): fixed-stride records of 1024 - 16257 B
-    const bool xw_var = variant % 64 == 44 || variant % 64 == 47;
+    const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 48;
     const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
     if (xw_var && !xwalk) variant = walk_variant(mode, has_desc);
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
@@ -270,6 +270,11 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         // default shape (16 x 4): C2copy 0.772-0.853 ms (variant 16) -> 0.692 ms (17) -> 0.678 ms
         // (21; tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 / 17 stay selectable.
         const int cv = ctx->variant;
+        if (cv >= 49 && cv <= 54 && xcopy_fits(p)) {  // the transposed layout (experiments build)
+            hipError_t e = launch_xcopy(cv, p, s);
+            if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
+            return SMOL_OK;
+        }
         const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17) ? cv : 21;
         const int cshape = ctx->shape >= 0 ? ctx->shape : ((var == 17 || var == 21) ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);

@@ -123,6 +123,10 @@ hipError_t launch_stripe(int mode, const KParams& p, hipStream_t s);
 // Transposed walk (csum_xwalk.hip, variants 44 / 47 = whole field segments): fixed-stride packed
 // records of 1024-16257 bytes.
 bool xwalk_fits(const KParams& p);
+// Copy-emit on the transposed walk's layout (csum_xcopy.hip, variants 49 / 50 = persistent grid,
+// experiments build): fixed-stride records of 1024-1921 bytes.
+bool xcopy_fits(const KParams& p);
+hipError_t launch_xcopy(int variant, const KParams& p, hipStream_t s);
 hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s);
 
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).

@@ -68,7 +68,10 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // window, the fields patched in (csum_walk.h variant 38's decision, the wavefront's groups all on
 // their one record): a whole segment costs HBM a plain write where a 2-B store costs a
 // read-modify-write.  NOSTORE (variant 64 + v): emit computes every field value and stores none.
-template <int MODE, int R, bool NOSTORE, bool SEG>
+// PERSIST (variant 48, experiments build): a grid of the resident workgroups whose wavefronts step
+// over the batch, issuing the next step's loads as soon as this step's sums are taken (before its
+// finish and stores), so that no wavefront ends while its stores drain.
+template <int MODE, int R, bool NOSTORE, bool SEG, bool PERSIST = false>
 __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     using namespace xwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
@@ -82,39 +85,47 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     const int lane = wl & (G - 1);
     const int gw = wl / G;  // the group (record) within the wavefront
     const int gib = wv * R + gw;
-    const uint64_t rw0 = (logical_block(p.xcd_remap) * WAVES + (uint64_t)wv) * R;  // the wavefront's first record
-    if (rw0 >= p.n) return;
-    const uint32_t cnt = (uint32_t)(p.n - rw0 < (uint64_t)R ? p.n - rw0 : (uint64_t)R);
     const uint32_t len = p.len;
     const uint64_t stride = p.stride;
     // packed records share lines with their neighbours (each line is loaded once); with a gap every
     // record loads all its lines and sums them masked to its span
     const bool packed = stride == (uint64_t)len;
+    const uint64_t nwaves = PERSIST ? (uint64_t)gridDim.x * WAVES : 0;
+    uint64_t tw = logical_block(p.xcd_remap) * WAVES + (uint64_t)wv;  // the wavefront's step
+    if (tw * R >= p.n) return;
 
-    // ---- all loads of the wavefront's records (record j: chunks below nload_j of its line grid) ----
+    // ---- all loads of a step's records (record j: chunks below nload_j of its line grid) ----
     u32x4 v[NS][R];
     uint32_t head[R], nload[R];
-    const uint64_t wbase = ((uint64_t)p.buf + rw0 * stride) & ~127ull;
-    const uint32_t whi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wbase >> 32));
-    const uint32_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wbase);
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)whi << 32) | wlo), 0, 0x7fffffff, 0x00020000);
+    auto issue = [&](uint64_t t) {
+        const uint64_t r0 = t * R;
+        const uint32_t c = (uint32_t)(p.n - r0 < (uint64_t)R ? p.n - r0 : (uint64_t)R);
+        const uint64_t wbase = ((uint64_t)p.buf + r0 * stride) & ~127ull;
+        const uint32_t whi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wbase >> 32));
+        const uint32_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wbase);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)whi << 32) | wlo), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-        const uint64_t a0 = (uint64_t)p.buf + (rw0 + (uint64_t)j) * stride;
-        const uint64_t b = a0 & ~127ull;
-        head[j] = (uint32_t)(a0 - b);
-        const uint32_t nch = (uint32_t)j < cnt ? (uint32_t)(((a0 + len + 15) >> 4) - (b >> 4)) : 0u;
-        // packed: the line holding record j + 1's first byte is record j + 1's to load
-        const bool shared = packed && (uint32_t)j + 1 < cnt;
-        nload[j] = shared ? (uint32_t)((((a0 + stride) & ~127ull) - b) >> 4) : nch;
-        const int soff = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b - wbase));
+        for (int j = 0; j < R; ++j) {
+            const uint64_t a0 = (uint64_t)p.buf + (r0 + (uint64_t)j) * stride;
+            const uint64_t b = a0 & ~127ull;
+            head[j] = (uint32_t)(a0 - b);
+            const uint32_t nch = (uint32_t)j < c ? (uint32_t)(((a0 + len + 15) >> 4) - (b >> 4)) : 0u;
+            // packed: the line holding record j + 1's first byte is record j + 1's to load
+            const bool shared = packed && (uint32_t)j + 1 < c;
+            nload[j] = shared ? (uint32_t)((((a0 + stride) & ~127ull) - b) >> 4) : nch;
+            const int soff = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b - wbase));
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const uint32_t k = (uint32_t)(64 * s + wl);
-            v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, k < nload[j] ? 16u * k : 0x80000000u, soff, 2 /* nt */);
+            for (int s = 0; s < NS; ++s) {
+                const uint32_t k = (uint32_t)(64 * s + wl);
+                v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, k < nload[j] ? 16u * k : 0x80000000u, soff, 2 /* nt */);
+            }
         }
-    }
+    };
+    issue(tw);
+    for (;;) {
+    const uint64_t rw0 = tw * R;  // the wavefront's first record
+    const uint32_t cnt = (uint32_t)(p.n - rw0 < (uint64_t)R ? p.n - rw0 : (uint64_t)R);
     // ---- the windows: chunks 0 .. 15 of record j are lanes 0 .. 15 of load (0, j) ----
 #pragma unroll
     for (int j = 0; j < R; ++j)
@@ -168,6 +179,10 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
             acc[j] += x;
         }
     }
+    // the next step's loads, ahead of this step's finish and stores
+    const uint64_t tn = tw + nwaves;
+    const bool more = PERSIST && tn * R < p.n;
+    if (more) issue(tn);
     // ---- reduce-scatter: record j's sum to group j ----
     uint32_t tot = group_sum<G>(reduce_scatter<R, 32>(acc, wl)) - hs;
     // packed: the bytes of this record's last line, which record j + 1 loaded, are record offsets
@@ -232,6 +247,10 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
             finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, lane == 0 ? tot : 0u, rd, winb, hd, a0,
                                                                          r, lane);
     }
+    if (!more) break;
+    wave_lds_sync();  // the windows are rewritten by the next step
+    tw = tn;
+    }
 }
 
 // records per wavefront for a record length (0: not served)
@@ -244,6 +263,19 @@ static int xwalk_records(uint32_t len) {
 
 template <int R>
 static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams& p, hipStream_t s) {
+#ifdef SMOL_EXP
+    if (variant == 48) {  // persistent, next step's loads ahead (the resident workgroups)
+        const uint32_t cap = mode == MODE_VERIFY
+                                 ? resident_blocks((const void*)xwalk_kernel<MODE_VERIFY, R, false, false, true>,
+                                                   p.num_cu ? p.num_cu : 256u, blocks)
+                                 : resident_blocks((const void*)xwalk_kernel<MODE_EMIT, R, false, true, true>,
+                                                   p.num_cu ? p.num_cu : 256u, blocks);
+        const uint32_t b = blocks < cap ? blocks : cap;
+        if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, true>), dim3(b), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, true>), dim3(b), dim3(256), 0, s, p);
+        return;
+    }
+#endif
     const bool seg = variant % 64 == 47;
     if (mode == MODE_VERIFY) {
         hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);

@@ -119,6 +119,8 @@ def _run(eng, recs, copies_spec, caps=(0, 0, 0, 0, 0), shape=-1, fixed_stride=No
         eng.set_max_blocks(0)
     if n:  # the forced variant ran its own kernel (default: copy_kernel variant 21)
         want = ("csum_kernel", variant) if variant in (1, 8, 11, 16) else ("copy_kernel", 17 if variant == 17 else 21)
+        if variant in (49, 50) and fixed_stride and 1024 <= (fixed_len or fixed_stride) <= 1921:
+            want = ("copy_kernel", variant)  # the transposed layout (csum_xcopy.hip)
         assert (launched["kernel"], launched["variant"]) == want, (variant, launched)
     diff = np.nonzero(got != ref)[0]
     assert diff.size == 0, f"bytes differ at {diff[:8]} (got {got[diff[:8]]} want {ref[diff[:8]]})"
@@ -172,7 +174,7 @@ def _fixed_case(rng, n, L):
 
 
 @pytest.mark.parametrize("stride,length", [(384, 384), (385, 385), (1500, 1500), (1514, 1514), (2048, 1500),
-                                           (4001, 4001), (700, 400)])
+                                           (4001, 4001), (700, 400), (1921, 1921), (1030, 1024)])
 def test_copy_emit_fixed_stride_mixed(eng, stride, length):
     """Fixed-stride batches of mixed records with every kind of copy range, at odd strides, gaps
     between records (random bytes that must survive), a batch base off the line grid, batch sizes
@@ -183,11 +185,45 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
         # the default (17), a capped grid, the prefetch variant (1), the two-load variant (8), the
         # lane-shuffle variants (11, 16)
         for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (8, 0), (8, 7), (16, 0), (16, 7), (17, 0),
-                               (17, 7), (21, 0), (21, 7)):
+                               (17, 7), (21, 0), (21, 7), (49, 0), (50, 0)):
             if not eng.has(variant):
                 continue
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,
                  base=base, seed=n + variant)
+
+
+@pytest.mark.parametrize("variant", [49, 50])
+@pytest.mark.parametrize("stride,length", [(1500, 1500), (1505, 1500), (1024, 1024), (1921, 1921), (1337, 1337)])
+def test_xcopy_fast_layout(eng, stride, length, variant):
+    """Copy-emit variants 49 / 50 (the transposed layout, natural / persistent grid) where its fast layout applies: every record of a
+    wavefront has its payload from inside the header window to the record's end (IPv4 / IPv6, UDP /
+    TCP / ICMP, payloads at source offsets of every 4-byte phase); then the same batch with one record
+    in 37 copying a shorter range, so that some wavefronts take the generic path.  Bit-exact
+    against the oracle, statuses included."""
+    eng.need(variant)
+    rng = np.random.default_rng(stride * 7 + length)
+    for n, base in ((1, 0), (9, 3), (1029, 0), (4099, 17)):
+        recs, spec = [], []
+        for i in range(n):
+            k = i % 5
+            if k == 0:
+                recs.append(P.ipv4(V4A, V4B, 17, P.udp(7, 9, P.rand_bytes(rng, length - 28))))
+                spec.append((28, length - 28))
+            elif k == 1:
+                recs.append(P.ipv4(V4A, V4B, 6, P.tcp(7, 9, P.rand_bytes(rng, length - 44), doff=6)))
+                spec.append((44, length - 44))
+            elif k == 2:
+                recs.append(P.ipv6(V6A, V6B, 17, P.udp(7, 9, P.rand_bytes(rng, length - 48))))
+                spec.append((48, length - 48))
+            elif k == 3:
+                recs.append(P.ipv6(V6A, V6B, 58, P.icmp_echo(128, P.rand_bytes(rng, length - 48))))
+                spec.append((48, length - 48))
+            else:
+                recs.append(P.ipv4(V4A, V4B, 1, P.icmp_echo(8, P.rand_bytes(rng, length - 28))))
+                spec.append((20, length - 20))  # the copy covers the ICMP header and its checksum field
+        _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, base=base, seed=n)
+        mixed = [(c[0], c[1] - 5) if i % 37 == 5 else c for i, c in enumerate(spec)]
+        _run(eng, recs, mixed, fixed_stride=stride, fixed_len=length, variant=variant, base=base, seed=n + 1)
 
 
 COPY_VARIANTS = [-1, 1, 8, 11, 16, 17, 21]

@@ -677,6 +677,7 @@ WIDE_KERNELS = {
     42: ("csum_tile_kernel", 1520),
     44: ("xwalk_kernel", 16257),
     47: ("xwalk_kernel", 16257),
+    48: ("xwalk_kernel", 16257),
 }
 
 
