@@ -156,7 +156,7 @@ bool variant_built(int v) {
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 42 || v == 48 || (v >= 49 && v <= 54);
+           (v >= 31 && v <= 38) || v == 42 || v == 48 || (v >= 49 && v <= 55);
 #else
     return false;
 #endif
@@ -270,7 +270,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         // default shape (16 x 4): C2copy 0.772-0.853 ms (variant 16) -> 0.692 ms (17) -> 0.678 ms
         // (21; tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 / 17 stay selectable.
         const int cv = ctx->variant;
-        if (cv >= 49 && cv <= 54 && xcopy_fits(p)) {  // the transposed layout (experiments build)
+        if (cv >= 49 && cv <= 55 && xcopy_fits(p)) {  // the transposed layout (experiments build)
             hipError_t e = launch_xcopy(cv, p, s);
             if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
             return SMOL_OK;

@@ -120,12 +120,14 @@ __device__ __forceinline__ u32x4 gen_merge(const Rec& q, uint32_t k, const Gen& 
 // trip (its loads) instead of two (the descriptors, then the loads that need them).
 // EXPT (variants 51-53, timing only, wrong bytes): 1 source loads rounded down to 16 B instead of
 // 4; 2 no body stores; 4 the C2copy descriptors computed, not loaded (src_offset 1472 r, dst 28).
-// 8 (variant 54, exact): non-temporal body stores.
+// 8 (variant 54, exact): non-temporal body stores.  16 (variant 55, exact): the body chunks re-dealt
+// through LDS and stored walk-shaped, each store instruction covering 128 B of each of the 8 records.
 template <bool PERSIST, int EXPT = 0>
 __global__ __launch_bounds__(256) void xcopy_kernel(KParams p) {
     using namespace xcopy;
     __shared__ u32x4 win[GPB][WIN_CH];
     __shared__ uint32_t spanbuf[GPB];
+    __shared__ u32x4 stg[(EXPT & 16) ? WAVES : 1][(EXPT & 16) ? R : 1][64];  // EXPT 16: one half-step's body chunks
     const int wl = (int)(threadIdx.x & 63);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = wl & (G - 1);
@@ -244,6 +246,42 @@ __global__ __launch_bounds__(256) void xcopy_kernel(KParams p) {
         wave_lds_sync();
         // ---- body: shift, sum, store ----
         uint32_t acc[R];
+        if constexpr ((EXPT & 16) != 0) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) acc[j] = 0;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const int sj = (int)spanbuf[wv * R + j], hj = (int)hd[j];
+                    const uint32_t k = (uint32_t)(64 * s + wl);
+                    const bool in = k >= (uint32_t)WIN_CH && k < nb[j];
+                    const u32x4 lo = v[s][j];
+                    const uint32_t b = bsh[j];
+                    u32x4 m;
+                    m.x = __builtin_amdgcn_alignbyte(lo.y, lo.x, b);
+                    m.y = __builtin_amdgcn_alignbyte(lo.z, lo.y, b);
+                    m.z = __builtin_amdgcn_alignbyte(lo.w, lo.z, b);
+                    m.w = __builtin_amdgcn_alignbyte(vh[s][j], lo.w, b);
+                    if (in) acc[j] = sum_chunk(m, 16 * (int)k - hj, sj, acc[j]);
+                    stg[wv][j][wl] = m;
+                }
+                wave_lds_sync();
+                // lane l stores chunks 64 s + 8 i + (l % 8) of its group's record (l / 8)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t kk = (uint32_t)(8 * i + lane), k = (uint32_t)(64 * s) + kk;
+                    if (mine && k >= (uint32_t)WIN_CH && k < q.nch - 1) {
+                        const u32x4 m = stg[wv][gw][kk];
+                        const gu8 dst = (gu8)q.base + 16u * k;
+                        const int pos = 16 * (int)k - (int)q.head;
+                        if (!any_far) *(GMEM u32x4*)dst = m;
+                        else store_part(dst, m, 0, 16, f0b - pos, f1b - pos, f2b - pos);
+                    }
+                }
+                wave_lds_sync();  // the staging is rewritten by the next half-step
+            }
+        } else
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             acc[j] = 0;
@@ -403,6 +441,7 @@ hipError_t launch_xcopy(int variant, const KParams& p, hipStream_t s) {
         else if (variant == 52) hipLaunchKernelGGL((xcopy_kernel<false, 2>), dim3(b), dim3(256), 0, s, q);
         else if (variant == 53) hipLaunchKernelGGL((xcopy_kernel<false, 4>), dim3(b), dim3(256), 0, s, q);
         else if (variant == 54) hipLaunchKernelGGL((xcopy_kernel<false, 8>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 55) hipLaunchKernelGGL((xcopy_kernel<false, 16>), dim3(b), dim3(256), 0, s, q);
         else hipLaunchKernelGGL((xcopy_kernel<false>), dim3(b), dim3(256), 0, s, q);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -119,7 +119,7 @@ def _run(eng, recs, copies_spec, caps=(0, 0, 0, 0, 0), shape=-1, fixed_stride=No
         eng.set_max_blocks(0)
     if n:  # the forced variant ran its own kernel (default: copy_kernel variant 21)
         want = ("csum_kernel", variant) if variant in (1, 8, 11, 16) else ("copy_kernel", 17 if variant == 17 else 21)
-        if variant in (49, 50) and fixed_stride and 1024 <= (fixed_len or fixed_stride) <= 1921:
+        if variant in (49, 50, 55) and fixed_stride and 1024 <= (fixed_len or fixed_stride) <= 1921:
             want = ("copy_kernel", variant)  # the transposed layout (csum_xcopy.hip)
         assert (launched["kernel"], launched["variant"]) == want, (variant, launched)
     diff = np.nonzero(got != ref)[0]
@@ -192,7 +192,7 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
                  base=base, seed=n + variant)
 
 
-@pytest.mark.parametrize("variant", [49, 50])
+@pytest.mark.parametrize("variant", [49, 50, 55])
 @pytest.mark.parametrize("stride,length", [(1500, 1500), (1505, 1500), (1024, 1024), (1921, 1921), (1337, 1337)])
 def test_xcopy_fast_layout(eng, stride, length, variant):
     """Copy-emit variants 49 / 50 (the transposed layout, natural / persistent grid) where its fast layout applies: every record of a
