@@ -154,9 +154,9 @@ bool variant_built(int v) {
     }
 #ifdef SMOL_EXP
     const int b = v >= 64 ? v - 64 : v;
-    if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47;
+    if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 42 || v == 48 || (v >= 49 && v <= 55);
+           (v >= 31 && v <= 38) || v == 42 || v == 48 || (v >= 49 && v <= 56);
 #else
     return false;
 #endif
@@ -281,6 +281,12 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
     }
+    if (variant % 64 == 56 && has_desc && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs) {
+        hipError_t e = launch_dwalk(mode, variant, p, s);  // descriptor batches (experiments build)
+        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
+        return SMOL_OK;
+    }
+    if (variant % 64 == 56) variant = walk_variant(mode, has_desc);
     if (xwalk) {
         hipError_t e = launch_xwalk(mode, variant, p, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");

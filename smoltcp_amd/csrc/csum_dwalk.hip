@@ -1,0 +1,213 @@
+// Transposed walk over descriptor batches (variant 56, experiments build): emit / verify of records
+// of any length and layout, with the walk kernel's per-record parse and gates.
+//
+// A wavefront owns 8 consecutive descriptors, a group of 8 lanes per record for the parse and the
+// gates.  When the 8 records lie back to back in memory (C3: packed records), the wavefront streams
+// their whole span [first record's 128-B line, last record's end) with wave-contiguous loads: load
+// instruction i covers bytes 1024 i .. 1024 i + 1023 of the span, one 16-B chunk per lane, 8
+// instructions in flight.  A lane adds its chunk to accumulator j of every record j the
+// instruction overlaps (a wave-uniform test per record: an instruction covers at most a few), whole
+// when the chunk lies inside the record's checksummed span, masked otherwise; a reduce-scatter over
+// the wavefront then leaves record j's sum in group j (csum_xwalk.hip).  Records that do not lie
+// back to back are streamed one at a time the same way.  The headers come from a 256-B LDS window
+// per record, loaded (two instructions for the 8 records) and parsed before the sums, whose masks
+// need each record's span end.
+#include "csum_walk.h"
+
+namespace smolcsum {
+
+#ifdef SMOL_EXP
+
+namespace dwalk {
+
+constexpr int R = 8;       // records per wavefront
+constexpr int G = 8;       // lanes per record (parse, gates)
+constexpr int WAVES = 4;
+constexpr int GPB = WAVES * R;
+constexpr int WIN_CH = 16;  // the LDS window: 256 B from the record's 128-B line
+constexpr int U = 8;        // load instructions in flight per wavefront
+
+}  // namespace dwalk
+
+template <int MODE, bool NOSTORE>
+__global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
+    using namespace dwalk;
+    constexpr bool EMIT = MODE == MODE_EMIT;
+    __shared__ u32x4 win[GPB][WIN_CH];
+    __shared__ uint32_t spanbuf[GPB];
+    const int wl = (int)(threadIdx.x & 63);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = wl & (G - 1);
+    const int gw = wl / G;
+    const int gib = wv * R + gw;
+    const uint64_t rw0 = (logical_block(p.xcd_remap) * WAVES + (uint64_t)wv) * R;
+    if (rw0 >= p.n) return;
+    const uint32_t cnt = (uint32_t)(p.n - rw0 < (uint64_t)R ? p.n - rw0 : (uint64_t)R);
+    const uint64_t dummy = (uint64_t)p.dummy;
+
+    // ---- descriptors: lane j holds record j's ----
+    const u32x4 d = (uint32_t)wl < cnt ? *(gcv4)((uint64_t)p.desc + 16 * (rw0 + (uint64_t)wl)) : u32x4{0, 0, 0, 0};
+    // wave-uniform record extents
+    uint64_t A[R];
+    uint32_t L[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const uint64_t off = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)d.x, j) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)d.y, j) << 32);
+        A[j] = (uint64_t)p.buf + off;
+        L[j] = (uint32_t)j < cnt ? (uint32_t)__builtin_amdgcn_readlane((int)d.z, j) : 0u;
+    }
+    bool contig = true;  // the records lie back to back (and their span stays below 2 GiB)
+#pragma unroll
+    for (int j = 1; j < R; ++j)
+        if ((uint32_t)j < cnt) contig = contig && A[j] == A[j - 1] + L[j - 1];
+    const uint64_t span_lo = A[0] & ~127ull;
+    contig = contig && A[cnt - 1] + L[cnt - 1] - span_lo < (1ull << 31);
+
+    // ---- the windows: instruction w, lane l: record 4 w + l / 16, chunk l % 16 ----
+    const bool mine = (uint32_t)gw < cnt;
+    const uint64_t r = rw0 + (uint64_t)gw;
+    const uint64_t a0 = (uint64_t)p.buf + ((uint64_t)(uint32_t)__shfl((int)d.x, gw, 64) |
+                                           ((uint64_t)(uint32_t)__shfl((int)d.y, gw, 64) << 32));
+    const uint32_t len = (uint32_t)__shfl((int)d.z, gw, 64);
+    const uint32_t kind = desc_kind((uint32_t)__shfl((int)d.w, gw, 64));
+    const uint32_t hd = (uint32_t)(a0 & 127u);
+    {
+        u32x4 wc[2];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+            const int rec = 4 * w + wl / 16, c = wl % 16;
+            const uint64_t ra = (uint64_t)p.buf + ((uint64_t)(uint32_t)__shfl((int)d.x, rec, 64) |
+                                                   ((uint64_t)(uint32_t)__shfl((int)d.y, rec, 64) << 32));
+            const uint32_t rl = (uint32_t)__shfl((int)d.z, rec, 64);
+            const uint64_t rb = ra & ~127ull;
+            const bool in = (uint32_t)rec < cnt && rb + 16ull * (uint32_t)c < ra + rl;
+            wc[w] = ld16<true>((gcv4)(in ? rb + 16ull * (uint32_t)c : dummy));
+        }
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+            const int rec = 4 * w + wl / 16;
+            if ((uint32_t)rec < cnt) win[wv * R + rec][wl % 16] = wc[w];
+        }
+    }
+    wave_lds_sync();
+    const uint8_t* winb = reinterpret_cast<const uint8_t*>(&win[gib][0]);
+    auto rd = [&](uint32_t o) -> uint32_t {
+        const uint32_t x = hd + o;
+        if (x < 16u * WIN_CH) return (uint32_t)winb[x];
+        return ld_byte_sync(a0 + o);
+    };
+    Geom g = Geom{};
+    if (mine) g = parse_geometry<false>(rd, len, kind, EMIT);
+    const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
+    if (lane == 0) spanbuf[gib] = mine && l4 ? g.span_end : 0u;
+    wave_lds_sync();
+    uint32_t S1[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) S1[j] = (uint32_t)__builtin_amdgcn_readfirstlane((int)spanbuf[wv * R + j]);
+
+    // ---- stream the span(s), summing each chunk into the records it overlaps ----
+    uint32_t acc[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[j] = 0;
+    const int nspans = contig ? 1 : (int)cnt;
+    for (int sp = 0; sp < nspans; ++sp) {
+        // span base (128-B line) and end, relative record bounds [lo_j, lo_j + S1_j)
+        uint64_t sb = span_lo, se = A[cnt - 1] + L[cnt - 1];
+        if (!contig) {
+            uint64_t aj = A[0];
+            uint32_t lj = L[0];
+#pragma unroll
+            for (int j = 1; j < R; ++j)
+                if (j == sp) {
+                    aj = A[j];
+                    lj = L[j];
+                }
+            sb = aj & ~127ull;
+            se = aj + lj;
+        }
+        const uint32_t bytes = (uint32_t)(se - sb);
+        int32_t lo[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) lo[j] = (int32_t)(A[j] - sb);
+        const uint32_t whi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sb >> 32));
+        const uint32_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sb);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)whi << 32) | wlo), 0, 0x7fffffff, 0x00020000);
+        const uint32_t ni = (bytes + 1023u) >> 10;
+        // U loads in flight, then their sums (measured: two sets in turn were slower, 0.90 against
+        // 0.835 ms for C3 verify: hipcc waits for every outstanding load at the loop head)
+        auto issue = [&](u32x4* v, uint32_t i0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t P = 1024u * (i0 + (uint32_t)u) + 16u * (uint32_t)wl;
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, P < bytes ? P : 0x80000000u, 0, 2 /* nt */);
+            }
+        };
+        for (uint32_t i0 = 0; i0 < ni; i0 += U) {
+            u32x4 v[U];
+            issue(v, i0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t I0 = 1024u * (i0 + (uint32_t)u);  // the instruction's first byte
+                if (i0 + (uint32_t)u >= ni) break;
+                const int pos0 = (int)(I0 + 16u * (uint32_t)wl);
+                const u32x4 c = v[u];
+                const uint32_t whole = add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u))));
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    // wave-uniform: does the instruction overlap record j's span?
+                    const bool rel = (contig || j == sp) && S1[j] > 0 && lo[j] < (int32_t)(I0 + 1024u) &&
+                                     lo[j] + (int32_t)S1[j] > (int32_t)I0;
+                    if (rel) {
+                        const int pos = pos0 - lo[j];  // the chunk's start relative to record j
+                        uint32_t x = 0;
+                        if (pos >= 0 && pos + 16 <= (int)S1[j]) x = whole;
+                        else if (pos + 16 > 0 && pos < (int)S1[j]) x = sum_masked_words(c, -pos, (int)S1[j] - pos, 0u);
+                        acc[j] += x;
+                    }
+                }
+            }
+        }
+    }
+    // ---- reduce-scatter: record j's sum to group j ----
+    uint32_t a4[4], a2[2];
+    const bool up32 = (wl & 32) != 0, up16 = (wl & 16) != 0, up8 = (wl & 8) != 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        a4[i] = (up32 ? acc[i + 4] : acc[i]) + (uint32_t)__shfl_xor((int)(up32 ? acc[i] : acc[i + 4]), 32, 64);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+        a2[i] = (up16 ? a4[i + 2] : a4[i]) + (uint32_t)__builtin_amdgcn_ds_swizzle((int)(up16 ? a4[i] : a4[i + 2]), 0x401F);
+    const uint32_t a1 = (up8 ? a2[1] : a2[0]) +
+                        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(up8 ? a2[0] : a2[1]), 0x128, 0xF, 0xF, false);
+    // ---- finish: the walk kernel's gates ----
+    if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane);
+}
+
+#endif  // SMOL_EXP
+
+hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) {
+#ifdef SMOL_EXP
+    const uint64_t per = (uint64_t)dwalk::GPB;
+    note_launch(KERN_XWALK, (uint32_t)variant, 8, 0);
+    const uint64_t span = kMaxGridBlocks * per;
+    for (uint64_t i0 = 0; i0 < p.n; i0 += span) {
+        KParams q = p;
+        q.n = p.n - i0 < span ? p.n - i0 : span;
+        q.desc = p.desc + i0;
+        if (p.status) q.status = p.status + i0;
+        const uint32_t b = grid_blocks((q.n + per - 1) / per, kMaxGridBlocks);
+        if (mode == MODE_VERIFY) hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false>), dim3(b), dim3(256), 0, s, q);
+        else if (variant >= 64) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, true>), dim3(b), dim3(256), 0, s, q);
+        else hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false>), dim3(b), dim3(256), 0, s, q);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+#else
+    return hipErrorInvalidValue;
+#endif
+}
+
+}  // namespace smolcsum

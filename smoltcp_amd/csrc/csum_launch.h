@@ -126,6 +126,8 @@ bool xwalk_fits(const KParams& p);
 // Copy-emit on the transposed walk's layout (csum_xcopy.hip, variants 49 / 50 = persistent grid,
 // experiments build): fixed-stride records of 1024-1921 bytes.
 bool xcopy_fits(const KParams& p);
+// The transposed walk over descriptor batches (csum_dwalk.hip, variant 56, experiments build).
+hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s);
 hipError_t launch_xcopy(int variant, const KParams& p, hipStream_t s);
 hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s);
 

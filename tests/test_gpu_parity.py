@@ -42,13 +42,17 @@ def _dev(buf: np.ndarray):
 
 
 def _run_records(eng, records, kinds, caps=CAPS_DEFAULT, gap_seed=None, shape=-1, max_blocks=0,
-                 base_pad=0):
-    """Verify and emit `records` on the device and on the oracle; assert identical results."""
+                 base_pad=0, variant=-1, order=None):
+    """Verify and emit `records` on the device and on the oracle; assert identical results.
+    `order`: a permutation of the descriptors (records stay where `pack` put them)."""
     rng = np.random.default_rng(gap_seed) if gap_seed is not None else None
     buf, offs, lens = P.pack(records, gap_rng=rng, base_pad=base_pad)
-    kinds = np.broadcast_to(np.asarray(kinds, dtype=np.uint8), (len(records),))
+    kinds = np.broadcast_to(np.asarray(kinds, dtype=np.uint8), (len(records),)).copy()
+    if order is not None:
+        offs, lens, kinds = np.asarray(offs)[order], np.asarray(lens)[order], kinds[order]
     eng.set_shape(shape)
     eng.set_max_blocks(max_blocks)
+    eng.set_variant(variant)
     try:
         batch = E.Batch.from_records(offs, lens, kinds, "cuda:0")
         d = _dev(buf)
@@ -64,10 +68,13 @@ def _run_records(eng, records, kinds, caps=CAPS_DEFAULT, gap_seed=None, shape=-1
         diff = np.nonzero(got != ref)[0]
         assert diff.size == 0, f"emit bytes differ at {diff[:8]}"
         assert np.array_equal(est.cpu().numpy(), ref_est), "emit status differs"
+        if variant == 56 and len(records):
+            assert eng.last_launch()["variant"] == 56, eng.last_launch()
         return st, got, offs, lens
     finally:
         eng.set_shape(-1)
         eng.set_max_blocks(0)
+        eng.set_variant(-1)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -269,6 +276,51 @@ def _mixed_records(rng, n=240):
             recs.append(P.ipv4(s4, d4, 6, P.tcp(7, 9, pl), ihl=int(rng.integers(5, 16)),
                                options=None))
     return recs
+
+
+def test_dwalk_descriptor_batches(eng):
+    """The transposed walk over descriptor batches (variant 56, experiments build): packed records
+    (one wave-contiguous span per 8 records), gapped and shuffled descriptors (one span per record),
+    tiny and empty records, records of 20-60 KB, Ethernet / raw / malformed records, every caps
+    gate; verify statuses and emitted bytes against the oracle."""
+    eng.need(56)
+    rng = np.random.default_rng(56)
+    recs = _mixed_records(rng, 400)
+    for i in range(0, 400, 37):  # long records
+        recs[i] = P.ipv4(V4A, V4B, 6, P.tcp(1, 2, P.rand_bytes(rng, int(rng.integers(20000, 60000)))))
+    for i in range(5, 400, 41):  # tiny and empty records
+        recs[i] = P.rand_bytes(rng, int(rng.integers(0, 40)))
+    _run_records(eng, recs, E.KIND_IP, variant=56)
+    _run_records(eng, recs, E.KIND_IP, variant=56, gap_seed=56)
+    _run_records(eng, recs, E.KIND_IP, variant=56, order=rng.permutation(len(recs)))
+    _run_records(eng, [P.eth(r, 0x0800) for r in recs], E.KIND_ETH, variant=56, base_pad=3)
+    for caps in ((2, 3, 0, 1, 0), (1, 1, 1, 1, 1)):
+        _run_records(eng, recs, E.KIND_IP, caps=caps, variant=56, gap_seed=7)
+    # C3-like: synthetic TCP segments of U[64, 9000] B packed at odd offsets
+    n = 4099
+    lens = rng.integers(64, 9001, n).astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    total = int(offs[-1] + lens[-1]) + 16
+    buf = torch.zeros(total + 1, dtype=torch.uint8, device="cuda:0")
+    view = buf[1:]
+    batch = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0")
+    eng.synth(view, batch, E.SYNTH_TCP4, seed=3)
+    eng.emit(view, batch)
+    eng.corrupt(view, batch, every=7, seed=3)
+    host = view.cpu().numpy().copy()
+    desc = P.oracle_desc(offs, lens, E.KIND_IP)
+    eng.set_variant(56)
+    try:
+        st = eng.verify(view, batch).cpu().numpy()
+        eng.emit(view, batch)
+        got = view.cpu().numpy()
+    finally:
+        eng.set_variant(-1)
+    assert np.array_equal(st, oracle.batch_verify(host.copy(), desc, n))
+    ref = host.copy()
+    oracle.batch_emit(ref, desc, n)
+    assert np.array_equal(got, ref)
 
 
 def test_all_caps_combinations(eng):
