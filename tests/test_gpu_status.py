@@ -107,37 +107,38 @@ def test_raw_records_desc(eng):
 
 def test_raw_records_fixed_stride_and_copy_emit(eng):
     """A fixed-stride batch flagged raw (smol_csum_batch_t.flags): UDP datagrams whose user
-    checksums must survive emit — and copy-emit, whose payload copy still happens."""
-    n, L = 512, 1500
-    buf = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
-    plain = E.Batch.fixed(n, L, kind=E.KIND_IP)
-    eng.synth(buf, plain, E.SYNTH_UDP4, seed=78)
-    h = buf.cpu().numpy().copy()
-    h.reshape(n, L)[:, 26:28] = np.array([0xBE, 0xEF], np.uint8)  # the user's UDP checksum
-    batch = E.Batch.fixed(n, L, kind=E.KIND_IP, flags=E.REC_IPHDR_ONLY)
-    for variant in eng.avail((-1, 0, 1, 5)):
-        eng.set_variant(variant)
-        try:
-            d = torch.from_numpy(h.copy()).cuda()
-            st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
-            eng.emit(d, batch, status=st)
-            ref = h.copy()
-            rst = oracle.batch_emit(ref, None, n, L, L, oracle.kind_flags(E.KIND_IP, E.REC_IPHDR_ONLY))
-            got = d.cpu().numpy()
-            assert np.array_equal(got, ref), variant
-            assert np.array_equal(st.cpu().numpy(), rst) and (rst == E.ST_UNSUPPORTED).all()
-            assert (got.reshape(n, L)[:, 26:28] == [0xBE, 0xEF]).all()
-            vst = eng.verify(d, batch).cpu().numpy()
-            assert np.array_equal(vst, oracle.batch_verify(ref, None, n, L, L,
-                                                           oracle.kind_flags(E.KIND_IP, E.REC_IPHDR_ONLY)))
-            assert (vst & E.ST_ACCEPT).all()
-        finally:
-            eng.set_variant(-1)
+    checksums must survive emit — and copy-emit, whose payload copy still happens.  1500 B (walk
+    kernel emit, transposed-walk verify) and 2500 B (transposed walk for both)."""
+    for n, L in ((512, 2500), (512, 1500)):
+        buf = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        plain = E.Batch.fixed(n, L, kind=E.KIND_IP)
+        eng.synth(buf, plain, E.SYNTH_UDP4, seed=78)
+        h = buf.cpu().numpy().copy()
+        h.reshape(n, L)[:, 26:28] = np.array([0xBE, 0xEF], np.uint8)  # the user's UDP checksum
+        batch = E.Batch.fixed(n, L, kind=E.KIND_IP, flags=E.REC_IPHDR_ONLY)
+        for variant in eng.avail((-1, 0, 1, 5, 44, 47)):
+            eng.set_variant(variant)
+            try:
+                d = torch.from_numpy(h.copy()).cuda()
+                st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+                eng.emit(d, batch, status=st)
+                ref = h.copy()
+                rst = oracle.batch_emit(ref, None, n, L, L, oracle.kind_flags(E.KIND_IP, E.REC_IPHDR_ONLY))
+                got = d.cpu().numpy()
+                assert np.array_equal(got, ref), (variant, L)
+                assert np.array_equal(st.cpu().numpy(), rst) and (rst == E.ST_UNSUPPORTED).all()
+                assert (got.reshape(n, L)[:, 26:28] == [0xBE, 0xEF]).all()
+                vst = eng.verify(d, batch).cpu().numpy()
+                assert np.array_equal(vst, oracle.batch_verify(ref, None, n, L, L,
+                                                               oracle.kind_flags(E.KIND_IP, E.REC_IPHDR_ONLY)))
+                assert (vst & E.ST_ACCEPT).all()
+            finally:
+                eng.set_variant(-1)
     src = np.random.default_rng(5).integers(0, 256, n * 1472 + 16, dtype=np.uint8)
     copies = E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472)
     ref = h.copy()
     oracle.batch_copy_emit(ref, None, n, src, copies, L, L, oracle.kind_flags(E.KIND_IP, E.REC_IPHDR_ONLY))
-    for variant in eng.avail((-1, 1, 17)):
+    for variant in eng.avail((-1, 1, 17, 49, 55)):
         eng.set_variant(variant)
         try:
             d = torch.from_numpy(h.copy()).cuda()
