@@ -71,7 +71,9 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // PERSIST (variant 48, experiments build): a grid of the resident workgroups whose wavefronts step
 // over the batch, issuing the next step's loads as soon as this step's sums are taken (before its
 // finish and stores), so that no wavefront ends while its stores drain.
-template <int MODE, int R, bool NOSTORE, bool SEG, bool PERSIST = false>
+// NTS (experiments build): the segments stored non-temporal, always (variant 57) or on a wavefront
+// that holds an IPv4 record (58).
+template <int MODE, int R, bool NOSTORE, bool SEG, bool PERSIST = false, int NTS = 0>
 __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     using namespace xwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
@@ -232,12 +234,14 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
         if (mine)
             finish_gates<G, MODE, false, decltype(rd), 16 * WIN_CH, true, NOSTORE>(
                 p, g, lane == 0 ? tot : 0u, rd, winb, hd, a0, r, lane, winw, wsA, wsB);
+        const bool nts = NTS == 1 || (NTS == 2 && __any(mine && g.fam == 4));
         wave_lds_sync();
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
         const uint64_t wb = a0 & ~127ull;
         auto seg_store = [&](uint64_t d) {
             const u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - wb));
             if constexpr (NOSTORE) asm volatile("" ::"v"(x), "v"(d));
+            else if (nts) __builtin_nontemporal_store(x, (GMEM u32x2*)d);
             else *(GMEM u32x2*)d = x;
         };
         if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
@@ -264,6 +268,12 @@ static int xwalk_records(uint32_t len) {
 template <int R>
 static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams& p, hipStream_t s) {
 #ifdef SMOL_EXP
+    if (variant == 57 || variant == 58) {
+        if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
+        else if (variant == 57) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 2>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
     if (variant == 48) {  // persistent, next step's loads ahead (the resident workgroups)
         const uint32_t cap = mode == MODE_VERIFY
                                  ? resident_blocks((const void*)xwalk_kernel<MODE_VERIFY, R, false, false, true>,
