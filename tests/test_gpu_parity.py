@@ -751,7 +751,8 @@ def test_wide_record_kernels(eng, variant):
     if lmax > 1520:  # every records-per-wavefront form, at both ends of its range
         lens += [(E.SYNTH_V6MIX, E.KIND_IP, 1777), (E.SYNTH_TCP4, E.KIND_IP, 1921), (E.SYNTH_UDP4, E.KIND_IP, 1922),
                  (E.SYNTH_V6MIX, E.KIND_IP, 3001), (E.SYNTH_TCP4, E.KIND_IP, 3969), (E.SYNTH_ETH_TCP4, E.KIND_ETH, 3970),
-                 (E.SYNTH_UDP4, E.KIND_IP, 8065), (E.SYNTH_V6MIX, E.KIND_IP, 8066), (E.SYNTH_TCP4, E.KIND_IP, lmax)]
+                 (E.SYNTH_UDP4, E.KIND_IP, 8065), (E.SYNTH_V6MIX, E.KIND_IP, 8066), (E.SYNTH_TCP4, E.KIND_IP, lmax),
+                 (E.SYNTH_UDP4, E.KIND_RAW, 2000)]
     for profile, kind, L in lens:
         for n, off in ((1, 0), (7, 3), (8, 0), (9, 64), (257, 1), (4099 if L < 4000 else 1029, 17)):
             host = np.zeros(off + n * L + 128, dtype=np.uint8)
