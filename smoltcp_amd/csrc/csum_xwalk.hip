@@ -23,9 +23,12 @@
 //    this wavefront, added to that record, which does not load the line (the line holding record
 //    j + 1's first byte is loaded once, as record j + 1's first chunk: csum_walk.h shared_from).
 //
-// Measured (profiles/r05_experiments/xwalk_*.txt): the other forms tried, a 64-bit-address load from
-// the dummy line for out-of-range chunks, a persistent grid (one wavefront steps over the batch 8
-// records at a time) and 5 wavefronts per SIMD (96 VGPRs), were all slower.
+// Measured (profiles/r05_experiments/xwalk_*.jsonl): the other forms tried, a
+// 64-bit-address load from the dummy line for out-of-range chunks, a persistent grid (one wavefront
+// steps over the batch 8 records at a time, with or without the next step's loads issued ahead:
+// PERSIST, variant 48) and 5 wavefronts per SIMD (96 VGPRs), were all slower.  The library uses it
+// where it beats the walk kernel (csum_api.cpp xwalk_auto): verify from 1473 B packed / 1666 B
+// gapped, emit from 1666 B, up to 10000 B.
 #include "csum_walk.h"
 
 namespace smolcsum {
