@@ -76,7 +76,10 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // finish and stores), so that no wavefront ends while its stores drain.
 // NTS (experiments build): the segments stored non-temporal, always (variant 57) or on a wavefront
 // that holds an IPv4 record (58).
-template <int MODE, int R, bool NOSTORE, bool SEG, bool PERSIST = false, int NTS = 0>
+// HALF (variant 59, experiments build; R = 8, records of at most 1409 B, whose line-grid span fits
+// 96 chunks): a record's second KiB is half an instruction, two records per instruction, so a
+// wavefront issues 12 loads instead of 16.
+template <int MODE, int R, bool NOSTORE, bool SEG, bool PERSIST = false, int NTS = 0, bool HALF = false>
 __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     using namespace xwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
@@ -100,7 +103,9 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     if (tw * R >= p.n) return;
 
     // ---- all loads of a step's records (record j: chunks below nload_j of its line grid) ----
+    static_assert(!HALF || R == 8, "HALF: 8 records per wavefront");
     u32x4 v[NS][R];
+    u32x4 vq[R / 2 > 0 ? R / 2 : 1];  // HALF: instruction q, lanes 0-31 / 32-63: chunks 64 .. 95 of records 2q / 2q + 1
     uint32_t head[R], nload[R];
     auto issue = [&](uint64_t t) {
         const uint64_t r0 = t * R;
@@ -121,9 +126,21 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
             nload[j] = shared ? (uint32_t)((((a0 + stride) & ~127ull) - b) >> 4) : nch;
             const int soff = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b - wbase));
 #pragma unroll
-            for (int s = 0; s < NS; ++s) {
+            for (int s = 0; s < (HALF ? 1 : NS); ++s) {
                 const uint32_t k = (uint32_t)(64 * s + wl);
                 v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, k < nload[j] ? 16u * k : 0x80000000u, soff, 2 /* nt */);
+            }
+        }
+        if constexpr (HALF) {
+#pragma unroll
+            for (int q = 0; q < R / 2; ++q) {
+                const bool hi = wl >= 32;
+                const uint32_t k = 64u + (uint32_t)(wl & 31);
+                const uint64_t bA = ((uint64_t)p.buf + (r0 + 2ull * q) * stride) & ~127ull;
+                const uint64_t bB = ((uint64_t)p.buf + (r0 + 2ull * q + 1) * stride) & ~127ull;
+                const uint32_t off = (uint32_t)((hi ? bB : bA) - wbase);
+                const uint32_t nl = hi ? nload[2 * q + 1] : nload[2 * q];
+                vq[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, k < nl ? off + 16u * k : 0x80000000u, 0, 2 /* nt */);
             }
         }
     };
@@ -168,20 +185,36 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     // Chunks below kend_j (the loaded chunks up to the span's end) are summed whole; the lane whose
     // chunk holds the span's end takes the bytes past it out again.  The bytes before the record in
     // its first line (hs) come out after the reduction.
-    uint32_t acc[R];
+    uint32_t acc[R], kend[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         acc[j] = 0;
         const int hj = (int)head[j], sj = span[j];
-        const uint32_t kend = min(nload[j], (uint32_t)(hj + sj + 15) >> 4);
+        kend[j] = min(nload[j], (uint32_t)(hj + sj + 15) >> 4);
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
+        for (int s = 0; s < (HALF ? 1 : NS); ++s) {
             const uint32_t k = (uint32_t)(64 * s + wl);
             const u32x4 c = v[s][j];
             const int pos = 16 * (int)k - hj;
-            uint32_t x = k < kend ? add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u)))) : 0u;
-            if (k < kend && pos + 16 > sj) x -= sum_masked_words(c, sj - pos, 16, 0u);
+            uint32_t x = k < kend[j] ? add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u)))) : 0u;
+            if (k < kend[j] && pos + 16 > sj) x -= sum_masked_words(c, sj - pos, 16, 0u);
             acc[j] += x;
+        }
+    }
+    if constexpr (HALF) {
+#pragma unroll
+        for (int q = 0; q < R / 2; ++q) {
+            const bool hi = wl >= 32;
+            const uint32_t k = 64u + (uint32_t)(wl & 31);
+            const int hj = (int)(hi ? head[2 * q + 1] : head[2 * q]);
+            const int sj = hi ? span[2 * q + 1] : span[2 * q];
+            const uint32_t ke = hi ? kend[2 * q + 1] : kend[2 * q];
+            const u32x4 c = vq[q];
+            const int pos = 16 * (int)k - hj;
+            uint32_t x = k < ke ? add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u)))) : 0u;
+            if (k < ke && pos + 16 > sj) x -= sum_masked_words(c, sj - pos, 16, 0u);
+            acc[2 * q] += hi ? 0u : x;
+            acc[2 * q + 1] += hi ? x : 0u;
         }
     }
     // the next step's loads, ahead of this step's finish and stores
@@ -271,6 +304,14 @@ static int xwalk_records(uint32_t len) {
 template <int R>
 static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams& p, hipStream_t s) {
 #ifdef SMOL_EXP
+    if constexpr (R == 8) {
+        if (variant == 59 && p.len <= 1409) {
+            if (mode == MODE_VERIFY)
+                hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, 8, false, false, false, 0, true>), dim3(blocks), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, 8, false, true, false, 0, true>), dim3(blocks), dim3(256), 0, s, p);
+            return;
+        }
+    }
     if (variant == 57 || variant == 58) {
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
         else if (variant == 57) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);

@@ -730,6 +730,7 @@ WIDE_KERNELS = {
     44: ("xwalk_kernel", 16257),
     47: ("xwalk_kernel", 16257),
     48: ("xwalk_kernel", 16257),
+    59: ("xwalk_kernel", 16257),
 }
 
 
