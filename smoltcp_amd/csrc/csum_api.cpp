@@ -105,18 +105,22 @@ int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc
 
 // Round 5: the transposed walk (csum_xwalk.hip, variant 47: emit with whole field segments) for
 // fixed-stride records where it beats the walk kernel.  Verify / emit of synthetic IPv4/UDP over
-// ~1.5 GB, R = 4 batches in turn, one box (tools/exp_r05_vlen.py, profiles/r05_experiments/
-// xwalk_vs_walk_packed.jsonl, xwalk_vs_walk_gap64.jsonl), walk / transposed walk time, packed:
-//   length   1024 1320 1472 1500 1600 1700 1921 2500 3969 5000 8065 9000 12000 16257
-//   verify   0.89 0.96 1.00 1.05 0.99 1.78 1.55 2.27 1.51 1.50 1.04 1.05  0.99  0.98
-//   emit     1.01 0.96 0.97 0.94 0.96 1.68 1.53 2.10 1.44 1.39 1.01 1.08  1.00  1.00
-// and with 64-B gaps verify 0.91 (1024) 0.92 (1320) 1.00 (1500) 1.72 (1700) 2.22 (2500) 1.49 (5000)
-// 1.06 (9000) 1.00 (12000), emit within 2 % of that.  The walk kernel's shapes leave lanes idle from
-// 1666 B (8 x 7 x 2 chunks no longer hold a record); 1500 B packed is a weak spot of its line grid.
+// ~1.5 GB, R = 4 batches in turn, one box per file (tools/exp_r05_vlen.py, profiles/r05_experiments/
+// xwalk_vs_walk_packed.jsonl, xwalk_vs_walk_gap64.jsonl, xwalk_verify_fine.jsonl,
+// xwalk_line_aligned.jsonl), walk / transposed walk time, packed:
+//   length   1024 1320 1472 1500 1536 1600 1700 1792 1921 2048 2500 3969 4096 5000 8065 8192 9000 12000
+//   verify   0.89 0.96 1.00 1.03 0.98 1.00 1.78 1.55 1.55 2.27 2.27 1.51 1.26 1.50 1.04 0.93 1.05  0.99
+//   emit     1.01 0.96 0.97 0.94 0.97 0.96 1.68 1.54 1.53 2.12 2.10 1.44 1.15 1.39 1.01 0.94 1.08  1.00
+// verify 1473-1665 B (every 20-50 B): 1.02-1.04 except 1536 (0.98) and 1600 (1.00); with 64-B gaps
+// verify 0.91 (1024) 0.92 (1320) 1.00 (1500) 1.72 (1700) 2.22 (2500) 1.49 (5000) 1.06 (9000) 1.00
+// (12000), emit within 2 % of that.  The walk kernel's shapes leave lanes idle from 1666 B (8 x 7
+// x 2 chunks no longer hold a record) and fit whole 128-B lines exactly at multiples of 128 B; past
+// 8065 B the transposed walk takes one record per wavefront and the two trade places by length.
 bool xwalk_auto(int mode, const smol_csum_batch_t* b) {
-    if (b->desc || b->stride < b->len) return false;
-    const uint32_t lo = (mode == MODE_VERIFY && b->stride == b->len) ? 1473u : 1666u;
-    return (mode == MODE_VERIFY || mode == MODE_EMIT) && b->len >= lo && b->len <= 10000;
+    if (b->desc || b->stride < b->len || (mode != MODE_VERIFY && mode != MODE_EMIT)) return false;
+    const bool packed = b->stride == b->len;
+    if (b->len >= 1666) return b->len <= 8065;
+    return mode == MODE_VERIFY && packed && b->len >= 1473 && b->len % 128 != 0;
 }
 
 // The XCD block order (csum_launch.h xcd_block / xcd_chunk) when none is forced: the contiguous order

@@ -27,8 +27,8 @@
 // 64-bit-address load from the dummy line for out-of-range chunks, a persistent grid (one wavefront
 // steps over the batch 8 records at a time, with or without the next step's loads issued ahead:
 // PERSIST, variant 48) and 5 wavefronts per SIMD (96 VGPRs), were all slower.  The library uses it
-// where it beats the walk kernel (csum_api.cpp xwalk_auto): verify from 1473 B packed / 1666 B
-// gapped, emit from 1666 B, up to 10000 B.
+// where it beats the walk kernel (csum_api.cpp xwalk_auto): verify of packed records from 1473 B
+// (not multiples of 128 B below 1666 B), verify of gapped records and emit from 1666 B, up to 8065 B.
 #include "csum_walk.h"
 
 namespace smolcsum {

@@ -56,8 +56,8 @@ def test_last_launch_families(eng):
     X, W = "xwalk_kernel", "csum_kernel"
     for LL, stride, op, want in ((1320, 1320, "verify", (W, 5, 8)), (1500, 1501, "verify", (W, 5, 8)),
                                  (2500, 2500, "emit", (X, 47, 16)), (2500, 2500, "verify", (X, 47, 16)),
-                                 (1500, 1500, "emit", (W, 39, 8)), (9000, 9000, "verify", (X, 47, 64)),
-                                 (9000, 9000, "emit", (X, 47, 64)), (12000, 12000, "emit", (W, 39, None)),
+                                 (1500, 1500, "emit", (W, 39, 8)), (9000, 9000, "verify", (W, 5, None)),
+                                 (8000, 8000, "emit", (X, 47, 32)), (1536, 1536, "verify", (W, 5, 8)), (12000, 12000, "emit", (W, 39, None)),
                                  (12000, 12000, "verify", (W, 5, None)), (2500, 2564, "emit", (X, 47, 16)),
                                  (1500, 1564, "verify", (W, 5, 8)), (1700, 1764, "verify", (X, 47, 8))):
         bb = E.Batch.fixed(8, stride, LL, E.KIND_IP)
