@@ -103,8 +103,9 @@ int smol_csum_tool_field_probe_list(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64
                                     const uint32_t* d_piece_first, int flags, void* stream);
 /* A separate store pass (experiments: what emit's field stores cost outside the read stream):
  * for i < n, the big-endian 2-byte value d_vals[i] at byte offset d_addrs[i] of the buffer, one
- * thread per store.  `flags` bit 0: non-temporal stores; bit 1: instead write the whole aligned
- * 64-byte segment holding the offset (the value repeated: a timing probe, the bytes change). */
+ * thread per store.  `flags` bit 0: non-temporal stores; bits 1 / 2 / 3: instead write the whole
+ * aligned 64-byte segment / 32-byte sector / 128-byte line holding the offset (the value repeated: a
+ * timing probe, the bytes change). */
 int smol_csum_tool_field_scatter(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
                                  const uint16_t* d_vals, uint64_t n, int flags, void* stream);
 /* The launch shape the library picks for a verify over an implicit batch of `len`-byte records. */

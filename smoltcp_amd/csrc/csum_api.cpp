@@ -578,10 +578,10 @@ int smol_csum_tool_field_probe_list(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64
 
 int smol_csum_tool_field_scatter(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
                                  const uint16_t* d_vals, uint64_t n, int flags, void* stream) {
-    if (!ctx || !d_buf || (n && (!d_addrs || !d_vals)) || (flags & ~3) || n > (0xFFFFFFull << 8)) return SMOL_EINVAL;
+    if (!ctx || !d_buf || (n && (!d_addrs || !d_vals)) || (flags & ~15) || n > (0xFFFFFFull << 8)) return SMOL_EINVAL;
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
-    hipError_t e = launch_field_scatter(d_buf, bytes, d_addrs, d_vals, n, flags & 3, (hipStream_t)stream);
+    hipError_t e = launch_field_scatter(d_buf, bytes, d_addrs, d_vals, n, flags & 15, (hipStream_t)stream);
     return e == hipSuccess ? SMOL_OK : hip_fail(e, "field-scatter kernel launch");
 }
 

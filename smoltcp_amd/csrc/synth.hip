@@ -368,13 +368,15 @@ __global__ __launch_bounds__(256) void field_scatter_kernel(uint8_t* buf, uint64
     const uint32_t v = vals[i];
     if (a + 2 > bytes) return;
     __attribute__((address_space(1))) uint8_t* g = (__attribute__((address_space(1))) uint8_t*)(buf + a);
-    if (nt & 2) {  // the aligned 64-B segment holding the field, written whole (timing probe: v repeated)
-        const uint64_t s0 = a & ~63ull;
-        if (s0 + 64 > bytes) return;
+    if (nt & 14) {  // the aligned 64-B segment (bit 1), 32-B sector (bit 2) or 128-B line (bit 3) holding
+                    // the field, written whole (timing probe: v repeated)
+        const uint64_t sz = (nt & 2) ? 64 : (nt & 4) ? 32 : 128;
+        const uint64_t s0 = a & ~(sz - 1);
+        if (s0 + sz > bytes) return;
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const uint32_t w = v * 0x10001u;
         const u32x4 x = {w, w, w, w};
-        for (int k = 0; k < 4; ++k) *(__attribute__((address_space(1))) u32x4*)(buf + s0 + 16 * k) = x;
+        for (uint64_t k = 0; k < sz / 16; ++k) *(__attribute__((address_space(1))) u32x4*)(buf + s0 + 16 * k) = x;
         return;
     }
     if (nt) {

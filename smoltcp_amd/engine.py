@@ -310,7 +310,8 @@ class ChecksumEngine:
     def field_scatter(self, buf, addrs, vals, nt: int = 0, stream=None):
         """A separate store pass (tooling, smol_csum_tool_field_scatter): the big-endian u16 `vals[i]`
         at byte offset `addrs[i]` (device int64 / uint16-as-int16 tensors) of `buf`.  `nt`: the flags
-        (bit 0 non-temporal stores, bit 1 the whole 64-B segment instead)."""
+        (bit 0 non-temporal stores; bits 1 / 2 / 3 the whole 64-B segment / 32-B sector / 128-B line
+        instead)."""
         check(self._L.smol_csum_tool_field_scatter(self._h, buf.data_ptr(), buf.numel(), addrs.data_ptr(),
                                                  vals.data_ptr(), int(addrs.numel()), int(nt),
                                                  self._stream(stream)), "smol_csum_tool_field_scatter")

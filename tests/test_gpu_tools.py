@@ -40,6 +40,27 @@ def test_field_scatter(eng, nt):
     assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:8]
 
 
+@pytest.mark.parametrize("flags,size", [(2, 64), (4, 32), (8, 128)])
+def test_field_scatter_whole_shapes(eng, flags, size):
+    """The timing shapes of the scatter probe: the aligned 64-B segment / 32-B sector / 128-B line
+    holding each listed offset is overwritten whole with the value repeated; nothing else changes;
+    a shape that would run past the buffer is skipped."""
+    rng = np.random.default_rng(flags)
+    nbytes = 1 << 14
+    host = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    offs = np.array([0, 77, 1000, 4097, nbytes - 2], dtype=np.int64)
+    vals = np.array([0x1234, 0xABCD, 0x0F0F, 0x5A5A, 0x7777], dtype=np.uint16)
+    ref = host.copy()
+    for o, v in zip(offs, vals):
+        s0 = int(o) // size * size
+        if s0 + size <= nbytes:
+            ref[s0:s0 + size] = np.tile(np.array([v & 0xFF, v >> 8], np.uint8), size // 2)
+    d = torch.from_numpy(host.copy()).cuda()
+    eng.field_scatter(d, torch.from_numpy(offs).cuda(), torch.from_numpy(vals.view(np.int16)).cuda(), nt=flags)
+    got = d.cpu().numpy()
+    assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:8]
+
+
 def test_last_launch_families(eng):
     """The launched-kernel record names the kernel family and the variant each entry point ran."""
     n, L = 257, 1500

@@ -12,7 +12,10 @@ Timed, interleaved on one box:
   alone     K write passes back to back, per pass;
   in_read   K (write pass + a read-only stream over a 4.7-GB buffer) minus K read streams, per pass:
             what the writes cost when their write-back lands inside a read stream (emit).
-Usage: [SPACINGS=256,512,...] [N=2097152] [ROUNDS=3] exp_write_tax.py"""
+FORMS: field2 (2-B fields), seg32 / seg64 / seg128 (the aligned 32-B sector / 64-B segment / 128-B
+line holding the field, written whole).
+Usage: [SPACINGS=256,512,...] [FORMS=field2,seg64] [ORDERS=address,window8k,random] [N=2097152] [ROUNDS=3]
+       exp_write_tax.py"""
 import json
 import os
 import sys
@@ -79,7 +82,11 @@ def main():
     for rnd in range(rounds):
         for S in spacings:
             for oname, addrs in orders(S):
-                for form, flags in (("field2", 0), ("seg64", 2)):
+                if oname not in os.environ.get("ORDERS", "address,window8k,random").split(","):
+                    continue
+                forms = {"field2": 0, "seg32": 4, "seg64": 2, "seg128": 8}
+                for form in os.environ.get("FORMS", "field2,seg64").split(","):
+                    flags = forms[form]
                     alone = t_alone(addrs, flags)
                     r0, r1 = t_read(addrs, flags)
                     print(json.dumps({"round": rnd, "spacing": S, "order": oname, "form": form, "writes": N,
