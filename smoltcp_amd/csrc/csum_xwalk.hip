@@ -243,8 +243,9 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     if constexpr (EMIT && SEG) {
         // A segment that starts before the record also holds record r-1's last bytes: whole only
         // for packed records, when r-1 has no field in its last 64 bytes (its group says so:
-        // ok_tail) and r-1 is in this wavefront.  A record whose fields end 64 bytes or more before its end never reaches into
-        // r+1 with its own segments.
+        // ok_tail) and r-1 is in this wavefront.  A record whose fields end 64 bytes or more before
+        // its end never reaches into r+1 with its own segments, and r-1's segments then end before
+        // this record, so no two groups write one segment.
         uint32_t f[3], lo = NO_FIELD, hi = 0;
         emit_fields(g, f);
 #pragma unroll
