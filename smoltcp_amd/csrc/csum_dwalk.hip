@@ -128,8 +128,14 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
         }
         const uint32_t bytes = (uint32_t)(se - sb);
         int32_t lo[R];
+        int32_t ifst[R], ilst[R];  // the span's load instructions that overlap record j's sum (empty: 0, -1)
 #pragma unroll
-        for (int j = 0; j < R; ++j) lo[j] = (int32_t)(A[j] - sb);
+        for (int j = 0; j < R; ++j) {
+            lo[j] = (int32_t)(A[j] - sb);
+            const bool in = (contig || j == sp) && S1[j] > 0;
+            ifst[j] = in ? lo[j] >> 10 : 0;
+            ilst[j] = in ? (lo[j] + (int32_t)S1[j] - 1) >> 10 : -1;
+        }
         const uint32_t whi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sb >> 32));
         const uint32_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sb);
         const __amdgpu_buffer_rsrc_t rs =
@@ -157,8 +163,8 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     // wave-uniform: does the instruction overlap record j's span?
-                    const bool rel = (contig || j == sp) && S1[j] > 0 && lo[j] < (int32_t)(I0 + 1024u) &&
-                                     lo[j] + (int32_t)S1[j] > (int32_t)I0;
+                    const int32_t ii = (int32_t)(i0 + (uint32_t)u);
+                    const bool rel = ii >= ifst[j] && ii <= ilst[j];
                     if (rel) {
                         const int pos = pos0 - lo[j];  // the chunk's start relative to record j
                         uint32_t x = 0;
