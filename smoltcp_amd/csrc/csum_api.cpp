@@ -101,7 +101,15 @@ int walk_variant(int mode, bool has_desc) {
     if (!has_desc) return mode == MODE_EMIT ? 39 : 5;
     return mode == MODE_EMIT ? 1 : mode == MODE_VERIFY ? 13 : 5;
 }
-int auto_variant(int mode, bool has_desc) { return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc); }
+// Round 5: verify over descriptor batches runs dwalk_kernel's per-group walk (variant 60, csum_dwalk.hip:
+// 8 records per wavefront, parse first, 8 lanes x 4 chunks per step on the line grid, 7 waves / SIMD):
+// C3 0.793 -> 0.742 ms, 64-1500-B records 0.343 -> 0.185 ms (tools/exp_r05_desc.py,
+// profiles/r05_experiments/dwalk_layouts.jsonl).  Its emit form lost to the tile kernel (0.958 vs
+// 0.937 ms on C3), which stays.
+int auto_variant(int mode, bool has_desc) {
+    if (mode == MODE_VERIFY && has_desc) return 60;
+    return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc);
+}
 
 // Round 5: the transposed walk (csum_xwalk.hip, variant 47: emit with whole field segments) for
 // fixed-stride records where it beats the walk kernel.  Verify / emit of synthetic IPv4/UDP over
@@ -149,11 +157,12 @@ int field_store_variant(int variant, bool has_desc) {
 }
 
 // The kernel variants this build runs (smol_csum_tool_variant_built).  The product library: the
-// defaults (walk 5 / 13 / 39, transposed walk 47, tile 7, copy 21) and one fallback each (copy 17;
-// walk 5 and 13 serve each other; 44 = 47 with 2-B field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
+// defaults (walk 5 / 39, transposed walk 47, descriptor walk 60, tile 7, copy 21) and one fallback
+// each (copy 17; walk 13 for NHC / data over descriptors and for forced variants; 44 = 47 with 2-B
+// field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
 bool variant_built(int v) {
     switch (v) {
-        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 47: return true;
+        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 47: case 60: return true;
         default: break;
     }
 #ifdef SMOL_EXP
@@ -238,12 +247,24 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     if (variant < 0) variant = (!d_addrs && xwalk_auto(mode, b)) ? 47 : auto_variant(mode, has_desc);
     if (mode == MODE_EMIT && (b->flags & SMOL_BATCH_FIELD_STORES)) variant = field_store_variant(variant, has_desc);
     // the stripe kernel (variant 42) serves emit / verify of packed fixed-stride records of 1024-1520 B
+    // a kernel that does not serve the batch falls back to the default of its kind (descriptor emit:
+    // the tile kernel; otherwise the walk kernel)
+    const int fallback = (mode == MODE_EMIT && has_desc && !d_addrs) ? 7 : walk_variant(mode, has_desc);
     const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
-    if (variant == 42 && !stripe) variant = walk_variant(mode, has_desc);
+    if (variant == 42 && !stripe) variant = fallback;
     // the transposed walk (variants 44 / 47, 64 + 44 / 47): fixed-stride records of 1024 - 16257 B
     const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 48 || variant == 57 || variant == 58 || variant == 59;
     const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
-    if (xw_var && !xwalk) variant = walk_variant(mode, has_desc);
+    if (xw_var && !xwalk) variant = fallback;
+    // descriptor-batch walks: 60 = verify default; 56 and 60's emit in the experiments build only
+#ifdef SMOL_EXP
+    const bool dw_var = variant % 64 == 56 || variant == 60;
+    const bool dwalk = dw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && has_desc && !d_addrs;
+#else
+    const bool dw_var = variant == 60;
+    const bool dwalk = dw_var && mode == MODE_VERIFY && has_desc && !d_addrs;
+#endif
+    if (dw_var && !dwalk) variant = fallback;
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
     if (tile_var && (mode == MODE_DATA || mode == MODE_COPY || d_addrs)) variant = walk_variant(mode, has_desc);
     const bool use_tile = variant == 3 || variant == 4 || variant == 7;
@@ -285,12 +306,11 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
         return SMOL_OK;
     }
-    if (variant % 64 == 56 && has_desc && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs) {
-        hipError_t e = launch_dwalk(mode, variant, p, s);  // descriptor batches (experiments build)
+    if (dwalk) {
+        hipError_t e = launch_dwalk(mode, variant, p, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         return SMOL_OK;
     }
-    if (variant % 64 == 56) variant = walk_variant(mode, has_desc);
     if (xwalk) {
         hipError_t e = launch_xwalk(mode, variant, p, s);
         if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
@@ -586,7 +606,9 @@ int smol_csum_tool_field_scatter(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t 
 }
 
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
-    const int v = auto_variant(MODE_VERIFY, has_desc != 0);
+    // the walk kernel's verify shape (descriptor batches: its variant 13, which serves them when the
+    // descriptor walk does not: NHC, data, forced variants)
+    const int v = has_desc ? walk_variant(MODE_VERIFY, true) : auto_variant(MODE_VERIFY, false);
     return auto_shape(len, has_desc != 0, line_grid(v), v);
 }
 
@@ -597,6 +619,7 @@ const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int h
         return (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? "csum_kernel" : "copy_kernel";
     }
     const int v = ctx->variant >= 0 ? ctx->variant : auto_variant(op, has_desc != 0);
+    if (v == 60 && op == MODE_VERIFY && has_desc) return "dwalk_kernel";
     const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY);
     return tile ? "csum_tile_kernel" : "csum_kernel";
 }

@@ -1,22 +1,30 @@
-// Transposed walk over descriptor batches (variant 56, experiments build): emit / verify of records
-// of any length and layout, with the walk kernel's per-record parse and gates.
+// Descriptor-batch walks (dwalk_kernel): verify / emit of records of any length and layout, with
+// the walk kernel's per-record parse and gates, 8 records per wavefront.
 //
-// A wavefront owns 8 consecutive descriptors, a group of 8 lanes per record for the parse and the
+// Variant 60 (the product's descriptor-batch verify since round 5): each group of 8 lanes streams
+// its own record on the record's 128-B line grid, U = 4 chunks per lane per step, after its header
+// window (two load instructions for the wavefront's 8 records) has been parsed, so that every chunk
+// is summed against the record's known span end.  64 VGPRs, 7 wavefronts per SIMD.  Measured
+// against the walk kernel's variant 13 (16 x 4, tools/exp_r05_desc.py,
+// profiles/r05_experiments/dwalk_layouts.jsonl): C3 verify 0.742 against 0.793 ms, gapped 0.742 /
+// 0.798, shuffled 0.760 / 0.815, records of 64-1500 B 0.185 / 0.343 ms.
+//
+// Variant 56 (experiments build):
+// a wavefront owns 8 consecutive descriptors, a group of 8 lanes per record for the parse and the
 // gates.  When the 8 records lie back to back in memory (C3: packed records), the wavefront streams
 // their whole span [first record's 128-B line, last record's end) with wave-contiguous loads: load
-// instruction i covers bytes 1024 i .. 1024 i + 1023 of the span, one 16-B chunk per lane, 8
+// instruction i covers bytes 1024 i .. 1024 i + 1023 of the span, one 16-B chunk per lane, U = 4
 // instructions in flight.  A lane adds its chunk to accumulator j of every record j the
-// instruction overlaps (a wave-uniform test per record: an instruction covers at most a few), whole
-// when the chunk lies inside the record's checksummed span, masked otherwise; a reduce-scatter over
-// the wavefront then leaves record j's sum in group j (csum_xwalk.hip).  Records that do not lie
-// back to back are streamed one at a time the same way.  The headers come from a 256-B LDS window
+// instruction overlaps (a wave-uniform test against record j's precomputed instruction range),
+// whole when the chunk lies inside the record's checksummed span, masked otherwise; a
+// reduce-scatter over the wavefront then leaves record j's sum in group j (csum_xwalk.hip).  A
+// wavefront whose records do not lie back to back streams them the walk kernel's way: each group
+// its own record, 8 lanes x U chunks per step.  The headers come from a 256-B LDS window
 // per record, loaded (two instructions for the 8 records) and parsed before the sums, whose masks
 // need each record's span end.
 #include "csum_walk.h"
 
 namespace smolcsum {
-
-#ifdef SMOL_EXP
 
 namespace dwalk {
 
@@ -25,11 +33,12 @@ constexpr int G = 8;       // lanes per record (parse, gates)
 constexpr int WAVES = 4;
 constexpr int GPB = WAVES * R;
 constexpr int WIN_CH = 16;  // the LDS window: 256 B from the record's 128-B line
-constexpr int U = 8;        // load instructions in flight per wavefront
+constexpr int U = 4;        // load instructions in flight per wavefront
 
 }  // namespace dwalk
 
-template <int MODE, bool NOSTORE>
+// GROUPS (variant 60): every wavefront streams its records the per-group way (the product's form).
+template <int MODE, bool NOSTORE, bool GROUPS = false>
 __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     using namespace dwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
@@ -106,35 +115,22 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
 #pragma unroll
     for (int j = 0; j < R; ++j) S1[j] = (uint32_t)__builtin_amdgcn_readfirstlane((int)spanbuf[wv * R + j]);
 
-    // ---- stream the span(s), summing each chunk into the records it overlaps ----
-    uint32_t acc[R];
+    uint32_t a1 = 0;  // this lane's part of its group's record sum
+    if (contig && !GROUPS) {
+        // ---- stream the span, summing each chunk into the records it overlaps ----
+        uint32_t acc[R];
 #pragma unroll
-    for (int j = 0; j < R; ++j) acc[j] = 0;
-    const int nspans = contig ? 1 : (int)cnt;
-    for (int sp = 0; sp < nspans; ++sp) {
+        for (int j = 0; j < R; ++j) acc[j] = 0;
         // span base (128-B line) and end, relative record bounds [lo_j, lo_j + S1_j)
-        uint64_t sb = span_lo, se = A[cnt - 1] + L[cnt - 1];
-        if (!contig) {
-            uint64_t aj = A[0];
-            uint32_t lj = L[0];
-#pragma unroll
-            for (int j = 1; j < R; ++j)
-                if (j == sp) {
-                    aj = A[j];
-                    lj = L[j];
-                }
-            sb = aj & ~127ull;
-            se = aj + lj;
-        }
+        const uint64_t sb = span_lo, se = A[cnt - 1] + L[cnt - 1];
         const uint32_t bytes = (uint32_t)(se - sb);
         int32_t lo[R];
-        int32_t ifst[R], ilst[R];  // the span's load instructions that overlap record j's sum (empty: 0, -1)
+        int32_t ifst[R], ilst[R];  // the load instructions that overlap record j's sum (empty: 0, -1)
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             lo[j] = (int32_t)(A[j] - sb);
-            const bool in = (contig || j == sp) && S1[j] > 0;
-            ifst[j] = in ? lo[j] >> 10 : 0;
-            ilst[j] = in ? (lo[j] + (int32_t)S1[j] - 1) >> 10 : -1;
+            ifst[j] = S1[j] > 0 ? lo[j] >> 10 : 0;
+            ilst[j] = S1[j] > 0 ? (lo[j] + (int32_t)S1[j] - 1) >> 10 : -1;
         }
         const uint32_t whi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sb >> 32));
         const uint32_t wlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sb);
@@ -143,29 +139,23 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
         const uint32_t ni = (bytes + 1023u) >> 10;
         // U loads in flight, then their sums (measured: two sets in turn were slower, 0.90 against
         // 0.835 ms for C3 verify: hipcc waits for every outstanding load at the loop head)
-        auto issue = [&](u32x4* v, uint32_t i0) {
+        for (uint32_t i0 = 0; i0 < ni; i0 += U) {
+            u32x4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t P = 1024u * (i0 + (uint32_t)u) + 16u * (uint32_t)wl;
                 v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, P < bytes ? P : 0x80000000u, 0, 2 /* nt */);
             }
-        };
-        for (uint32_t i0 = 0; i0 < ni; i0 += U) {
-            u32x4 v[U];
-            issue(v, i0);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t I0 = 1024u * (i0 + (uint32_t)u);  // the instruction's first byte
-                if (i0 + (uint32_t)u >= ni) break;
-                const int pos0 = (int)(I0 + 16u * (uint32_t)wl);
+                const int32_t ii = (int32_t)(i0 + (uint32_t)u);
+                if (ii >= (int32_t)ni) break;
+                const int pos0 = 1024 * ii + 16 * wl;
                 const u32x4 c = v[u];
                 const uint32_t whole = add_words(c.x, add_words(c.y, add_words(c.z, add_words(c.w, 0u))));
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
-                    // wave-uniform: does the instruction overlap record j's span?
-                    const int32_t ii = (int32_t)(i0 + (uint32_t)u);
-                    const bool rel = ii >= ifst[j] && ii <= ilst[j];
-                    if (rel) {
+                    if (ii >= ifst[j] && ii <= ilst[j]) {  // wave-uniform
                         const int pos = pos0 - lo[j];  // the chunk's start relative to record j
                         uint32_t x = 0;
                         if (pos >= 0 && pos + 16 <= (int)S1[j]) x = whole;
@@ -175,28 +165,51 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
                 }
             }
         }
+        // ---- reduce-scatter: record j's sum to group j ----
+        uint32_t a4[4], a2[2];
+        const bool up32 = (wl & 32) != 0, up16 = (wl & 16) != 0, up8 = (wl & 8) != 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            a4[i] = (up32 ? acc[i + 4] : acc[i]) + (uint32_t)__shfl_xor((int)(up32 ? acc[i] : acc[i + 4]), 32, 64);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            a2[i] = (up16 ? a4[i + 2] : a4[i]) + (uint32_t)__builtin_amdgcn_ds_swizzle((int)(up16 ? a4[i] : a4[i + 2]), 0x401F);
+        a1 = (up8 ? a2[1] : a2[0]) +
+             (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(up8 ? a2[0] : a2[1]), 0x128, 0xF, 0xF, false);
+    } else {
+        // ---- records not back to back: each group streams its own record on its line grid,
+        //      8 lanes x U chunks per step (the walk kernel's layout) ----
+        const int s1 = mine && l4 ? (int)g.span_end : 0;
+        const uint64_t base = a0 & ~127ull;
+        const uint32_t nch = (uint32_t)((int)hd + s1 + 15) >> 4;  // chunks up to the span's end
+        for (uint32_t c0 = 0; c0 < nch; c0 += (uint32_t)(G * U)) {
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = c0 + (uint32_t)(G * u + lane);
+                v[u] = ld16<true>((gcv4)(c < nch ? base + 16ull * c : dummy));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = c0 + (uint32_t)(G * u + lane);
+                const int pos = 16 * (int)c - (int)hd;
+                if (c < nch) {
+                    if (pos >= 0 && pos + 16 <= s1) a1 = add_words(v[u].x, add_words(v[u].y, add_words(v[u].z, add_words(v[u].w, a1))));
+                    else a1 = sum_masked_words(v[u], -pos, s1 - pos, a1);
+                }
+            }
+        }
     }
-    // ---- reduce-scatter: record j's sum to group j ----
-    uint32_t a4[4], a2[2];
-    const bool up32 = (wl & 32) != 0, up16 = (wl & 16) != 0, up8 = (wl & 8) != 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        a4[i] = (up32 ? acc[i + 4] : acc[i]) + (uint32_t)__shfl_xor((int)(up32 ? acc[i] : acc[i + 4]), 32, 64);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-        a2[i] = (up16 ? a4[i + 2] : a4[i]) + (uint32_t)__builtin_amdgcn_ds_swizzle((int)(up16 ? a4[i] : a4[i + 2]), 0x401F);
-    const uint32_t a1 = (up8 ? a2[1] : a2[0]) +
-                        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(up8 ? a2[0] : a2[1]), 0x128, 0xF, 0xF, false);
     // ---- finish: the walk kernel's gates ----
     if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane);
 }
 
-#endif  // SMOL_EXP
-
 hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) {
-#ifdef SMOL_EXP
+#ifndef SMOL_EXP
+    if (variant != 60 || mode != MODE_VERIFY) return hipErrorInvalidValue;  // the product's form
+#endif
     const uint64_t per = (uint64_t)dwalk::GPB;
-    note_launch(KERN_XWALK, (uint32_t)variant, 8, 0);
+    note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
     const uint64_t span = kMaxGridBlocks * per;
     for (uint64_t i0 = 0; i0 < p.n; i0 += span) {
         KParams q = p;
@@ -204,16 +217,18 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         q.desc = p.desc + i0;
         if (p.status) q.status = p.status + i0;
         const uint32_t b = grid_blocks((q.n + per - 1) / per, kMaxGridBlocks);
-        if (mode == MODE_VERIFY) hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false>), dim3(b), dim3(256), 0, s, q);
+        if (variant == 60 && mode == MODE_VERIFY)
+            hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false, true>), dim3(b), dim3(256), 0, s, q);
+#ifdef SMOL_EXP
+        else if (variant == 60) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true>), dim3(b), dim3(256), 0, s, q);
+        else if (mode == MODE_VERIFY) hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false>), dim3(b), dim3(256), 0, s, q);
         else if (variant >= 64) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, true>), dim3(b), dim3(256), 0, s, q);
         else hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false>), dim3(b), dim3(256), 0, s, q);
+#endif
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
-#else
-    return hipErrorInvalidValue;
-#endif
 }
 
 }  // namespace smolcsum

@@ -86,7 +86,7 @@ __device__ inline uint64_t logical_block(uint32_t xcd_remap) {
 // The kernel instantiation of the process's last checksum launch, packed kernel << 24 | variant << 16
 // | G << 8 | U (smol_csum_tool_last_launch): tests check that a forced variant runs the kernel it
 // names rather than a dispatch fallback.
-enum { KERN_WALK = 1, KERN_TILE = 2, KERN_COPY = 3, KERN_WALK_NHC = 4, KERN_XWALK = 5 };
+enum { KERN_WALK = 1, KERN_TILE = 2, KERN_COPY = 3, KERN_WALK_NHC = 4, KERN_XWALK = 5, KERN_DWALK = 6 };
 inline std::atomic<uint32_t> g_last_launch{0};
 inline void note_launch(uint32_t kern, uint32_t var, uint32_t g, uint32_t u) {
     g_last_launch.store(kern << 24 | (var & 0xffu) << 16 | (g & 0xffu) << 8 | (u & 0xffu),
@@ -126,7 +126,7 @@ bool xwalk_fits(const KParams& p);
 // Copy-emit on the transposed walk's layout (csum_xcopy.hip, variants 49 / 50 = persistent grid,
 // experiments build): fixed-stride records of 1024-1921 bytes.
 bool xcopy_fits(const KParams& p);
-// The transposed walk over descriptor batches (csum_dwalk.hip, variant 56, experiments build).
+// Descriptor-batch walks (csum_dwalk.hip): variant 60 = verify default; 56 / 60 emit: experiments.
 hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s);
 hipError_t launch_xcopy(int variant, const KParams& p, hipStream_t s);
 hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s);

@@ -337,11 +337,12 @@ class ChecksumEngine:
 
     def last_launch(self) -> dict:
         """The kernel instantiation of the process's last checksum launch: {"kernel": "csum_kernel" |
-        "csum_tile_kernel" | "copy_kernel" | "csum_kernel_nhc" | "xwalk_kernel", "variant": VAR, "G":
+        "csum_tile_kernel" | "copy_kernel" | "csum_kernel_nhc" | "xwalk_kernel" | "dwalk_kernel", "variant": VAR, "G":
         lanes per record, "U": chunks per lane per step (xwalk_kernel: 1-KiB loads per record)} (None
         before the first launch)."""
         w = int(self._L.smol_csum_tool_last_launch())
-        names = {1: "csum_kernel", 2: "csum_tile_kernel", 3: "copy_kernel", 4: "csum_kernel_nhc", 5: "xwalk_kernel"}
+        names = {1: "csum_kernel", 2: "csum_tile_kernel", 3: "copy_kernel", 4: "csum_kernel_nhc", 5: "xwalk_kernel",
+                 6: "dwalk_kernel"}
         if not w >> 24:
             return None
         return {"kernel": names.get(w >> 24, "?"), "variant": (w >> 16) & 0xff, "G": (w >> 8) & 0xff, "U": w & 0xff}

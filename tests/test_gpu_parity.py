@@ -57,6 +57,7 @@ def _run_records(eng, records, kinds, caps=CAPS_DEFAULT, gap_seed=None, shape=-1
         batch = E.Batch.from_records(offs, lens, kinds, "cuda:0")
         d = _dev(buf)
         st = eng.verify(d, batch, caps=caps).cpu().numpy()
+        launched_v = eng.last_launch()
         ref_st = P.oracle_verify_records(buf, offs, lens, kinds, caps)
         bad = np.nonzero(st != ref_st)[0]
         assert bad.size == 0, f"verify mismatch at {bad[:8]}: got {st[bad[:8]]} want {ref_st[bad[:8]]}"
@@ -68,8 +69,8 @@ def _run_records(eng, records, kinds, caps=CAPS_DEFAULT, gap_seed=None, shape=-1
         diff = np.nonzero(got != ref)[0]
         assert diff.size == 0, f"emit bytes differ at {diff[:8]}"
         assert np.array_equal(est.cpu().numpy(), ref_est), "emit status differs"
-        if variant == 56 and len(records):
-            assert eng.last_launch()["variant"] == 56, eng.last_launch()
+        if variant in (56, 60) and len(records):  # verify ran the descriptor walk it names
+            assert (launched_v["kernel"], launched_v["variant"]) == ("dwalk_kernel", variant), launched_v
         return st, got, offs, lens
     finally:
         eng.set_shape(-1)
@@ -278,24 +279,25 @@ def _mixed_records(rng, n=240):
     return recs
 
 
-def test_dwalk_descriptor_batches(eng):
+@pytest.mark.parametrize("variant", [56, 60])
+def test_dwalk_descriptor_batches(eng, variant):
     """The transposed walk over descriptor batches (variant 56, experiments build): packed records
     (one wave-contiguous span per 8 records), gapped and shuffled descriptors (one span per record),
     tiny and empty records, records of 20-60 KB, Ethernet / raw / malformed records, every caps
     gate; verify statuses and emitted bytes against the oracle."""
-    eng.need(56)
+    eng.need(variant)
     rng = np.random.default_rng(56)
     recs = _mixed_records(rng, 400)
     for i in range(0, 400, 37):  # long records
         recs[i] = P.ipv4(V4A, V4B, 6, P.tcp(1, 2, P.rand_bytes(rng, int(rng.integers(20000, 60000)))))
     for i in range(5, 400, 41):  # tiny and empty records
         recs[i] = P.rand_bytes(rng, int(rng.integers(0, 40)))
-    _run_records(eng, recs, E.KIND_IP, variant=56)
-    _run_records(eng, recs, E.KIND_IP, variant=56, gap_seed=56)
-    _run_records(eng, recs, E.KIND_IP, variant=56, order=rng.permutation(len(recs)))
-    _run_records(eng, [P.eth(r, 0x0800) for r in recs], E.KIND_ETH, variant=56, base_pad=3)
+    _run_records(eng, recs, E.KIND_IP, variant=variant)
+    _run_records(eng, recs, E.KIND_IP, variant=variant, gap_seed=56)
+    _run_records(eng, recs, E.KIND_IP, variant=variant, order=rng.permutation(len(recs)))
+    _run_records(eng, [P.eth(r, 0x0800) for r in recs], E.KIND_ETH, variant=variant, base_pad=3)
     for caps in ((2, 3, 0, 1, 0), (1, 1, 1, 1, 1)):
-        _run_records(eng, recs, E.KIND_IP, caps=caps, variant=56, gap_seed=7)
+        _run_records(eng, recs, E.KIND_IP, caps=caps, variant=variant, gap_seed=7)
     # C3-like: synthetic TCP segments of U[64, 9000] B packed at odd offsets
     n = 4099
     lens = rng.integers(64, 9001, n).astype(np.uint32)
@@ -310,7 +312,7 @@ def test_dwalk_descriptor_batches(eng):
     eng.corrupt(view, batch, every=7, seed=3)
     host = view.cpu().numpy().copy()
     desc = P.oracle_desc(offs, lens, E.KIND_IP)
-    eng.set_variant(56)
+    eng.set_variant(variant)
     try:
         st = eng.verify(view, batch).cpu().numpy()
         eng.emit(view, batch)

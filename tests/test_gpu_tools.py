@@ -94,7 +94,8 @@ def test_last_launch_families(eng):
     assert (ll["kernel"], ll["variant"]) == ("csum_tile_kernel", 2), ll
     eng.verify(buf, bd)
     ll = eng.last_launch()
-    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("csum_kernel", 13, 16, 4), ll
+    # descriptor-batch verify: the per-group descriptor walk (csum_dwalk.hip), 8 lanes x 4 chunks
+    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 60, 8, 4), ll
     src = torch.zeros(n * 1472 + 16, dtype=torch.uint8, device="cuda:0")
     cp = torch.from_numpy(E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472).view(np.uint8).copy()).cuda()
     eng.copy_emit(buf, b, src, cp)
