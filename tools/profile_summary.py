@@ -37,7 +37,7 @@ def kernel_role(name: str):
     """'emit' / 'verify' / 'data' for the checksum kernels, else None."""
     if re.search(r"copy_kernel<", name):  # csum_copy.hip: <G, U, IMPLICIT>, copy-emit only
         return "copy_emit"
-    m = re.search(r"xwalk_kernel<([^>]*)>", name)  # csum_xwalk.hip: <MODE, R, NOSTORE, SEG>
+    m = re.search(r"[xd]walk_kernel<([^>]*)>", name)  # csum_xwalk.hip <MODE, R, ...>, csum_dwalk.hip <MODE, ...>
     if m:
         return MODES.get(m.group(1).split(",")[0].strip())
     m = re.search(r"(csum_kernel|csum_tile_kernel)<([^>]*)>", name)
