@@ -101,14 +101,19 @@ int walk_variant(int mode, bool has_desc) {
     if (!has_desc) return mode == MODE_EMIT ? 39 : 5;
     return mode == MODE_EMIT ? 1 : mode == MODE_VERIFY ? 13 : 5;
 }
-// Round 5: verify over descriptor batches runs dwalk_kernel's per-group walk (variant 60, csum_dwalk.hip:
-// 8 records per wavefront, parse first, 8 lanes x 4 chunks per step on the line grid, 7 waves / SIMD):
-// C3 0.793 -> 0.742 ms, 64-1500-B records 0.343 -> 0.185 ms (tools/exp_r05_desc.py,
-// profiles/r05_experiments/dwalk_layouts.jsonl).  Its emit form lost to the tile kernel (0.958 vs
-// 0.937 ms on C3), which stays.
+// Round 5: verify over descriptor batches runs dwalk_kernel's per-group walk (csum_dwalk.hip: 8
+// records per wavefront, parse first, 8 lanes x 4 chunks per step on the line grid, 7 waves / SIMD):
+// C3 0.793 -> 0.742 ms, 64-1500-B records 0.343 -> 0.185 ms with non-temporal header windows
+// (variant 60, tools/exp_r05_desc.py, profiles/r05_experiments/dwalk_layouts.jsonl).  Variant 63
+// loads the header windows with the default cache policy, so that the stream's second read of those
+// lines and emit's field stores hit the L2: C3 bench (4 batch pairs in turn, one box, interleaved)
+// verify 0.742 -> 0.731 ms and emit 0.942 (tile 7) -> 0.896 ms, 5269 -> 5457 GiB/s
+// (profiles/r05_experiments/dwalk_cached_windows.txt); its emit beats the tile kernel on every
+// descriptor layout measured, 64-1500-B records 0.223 -> 0.184 ms.  The tile kernel stays the
+// descriptor-emit fallback (NHC emit runs the walk kernel).
 int auto_variant(int mode, bool has_desc) {
-    if (mode == MODE_VERIFY && has_desc) return 60;
-    return mode == MODE_EMIT && has_desc ? 7 : walk_variant(mode, has_desc);
+    if ((mode == MODE_VERIFY || mode == MODE_EMIT) && has_desc) return 63;
+    return walk_variant(mode, has_desc);
 }
 
 // Round 5: the transposed walk (csum_xwalk.hip, variant 47: emit with whole field segments) for
@@ -152,6 +157,8 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
     if (variant == 47) return 44;
+    if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
+    if (variant == 62) return 63;  // (63 stores 2-B fields only)
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
@@ -162,14 +169,14 @@ int field_store_variant(int variant, bool has_desc) {
 // field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
 bool variant_built(int v) {
     switch (v) {
-        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 47: case 60: return true;
+        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 47: case 60: case 63: return true;
         default: break;
     }
 #ifdef SMOL_EXP
     const int b = v >= 64 ? v - 64 : v;
-    if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56;
+    if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 40 || v == 42 || v == 48 || (v >= 49 && v <= 59);
+           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
 #else
     return false;
 #endif
@@ -177,7 +184,7 @@ bool variant_built(int v) {
 
 bool line_grid(int variant) {
     if (variant >= 64) variant -= 64;  // experiment variants without stores
-    if (variant >= 31 && variant <= 40) return true;
+    if ((variant >= 31 && variant <= 40) || variant == 12 || variant == 14) return true;
     return variant == 5 || variant == 6 || variant == 9 || variant == 10 || variant == 13 || variant == 19 ||
            (variant >= 23 && variant <= 29);
 }
@@ -256,13 +263,17 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 48 || variant == 57 || variant == 58 || variant == 59;
     const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
     if (xw_var && !xwalk) variant = fallback;
-    // descriptor-batch walks: 60 = verify default; 56 and 60's emit in the experiments build only
+    // descriptor-batch walks: 63 = verify / emit default (cached header windows), 60 = its
+    // non-temporal-window verify; 56, 60's emit and 61 / 62 (emit with whole field segments) in the
+    // experiments build only
 #ifdef SMOL_EXP
-    const bool dw_var = variant % 64 == 56 || variant == 60;
+    const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63;
+    if (variant % 64 == 61 && mode == MODE_VERIFY) variant = 60;  // an emit form of 60
+    if (variant == 62 && mode == MODE_VERIFY) variant = 63;      // an emit form of 63
     const bool dwalk = dw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && has_desc && !d_addrs;
 #else
-    const bool dw_var = variant == 60;
-    const bool dwalk = dw_var && mode == MODE_VERIFY && has_desc && !d_addrs;
+    const bool dw_var = variant == 60 || variant == 63;
+    const bool dwalk = dw_var && (mode == MODE_VERIFY || (mode == MODE_EMIT && variant == 63)) && has_desc && !d_addrs;
 #endif
     if (dw_var && !dwalk) variant = fallback;
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
@@ -619,7 +630,8 @@ const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int h
         return (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? "csum_kernel" : "copy_kernel";
     }
     const int v = ctx->variant >= 0 ? ctx->variant : auto_variant(op, has_desc != 0);
-    if (v == 60 && op == MODE_VERIFY && has_desc) return "dwalk_kernel";
+    if (has_desc && ((v == 60 && op == MODE_VERIFY) || (v == 63 && (op == MODE_VERIFY || op == MODE_EMIT))))
+        return "dwalk_kernel";
     const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY);
     return tile ? "csum_tile_kernel" : "csum_kernel";
 }

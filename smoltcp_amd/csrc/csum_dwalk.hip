@@ -1,7 +1,13 @@
 // Descriptor-batch walks (dwalk_kernel): verify / emit of records of any length and layout, with
 // the walk kernel's per-record parse and gates, 8 records per wavefront.
 //
-// Variant 60 (the product's descriptor-batch verify since round 5): each group of 8 lanes streams
+// Variant 63 (the product's descriptor-batch verify and emit since round 5) is variant 60 with the
+// header windows loaded with the default cache policy: the stream below reads those lines again
+// (non-temporal loads, line grid from the record's first line) and emit's field stores write them;
+// with the windows cached both hit the L2.  Measured (bench.py --config c3, 4 batch pairs in turn,
+// interleaved on one box): verify 0.742 -> 0.731 ms, emit 0.942 (tile kernel) -> 0.896 ms.
+//
+// Variant 60 (the descriptor-batch verify before variant 63): each group of 8 lanes streams
 // its own record on the record's 128-B line grid, U = 4 chunks per lane per step, after its header
 // window (two load instructions for the wavefront's 8 records) has been parsed, so that every chunk
 // is summed against the record's known span end.  64 VGPRs, 7 wavefronts per SIMD.  Measured
@@ -38,7 +44,12 @@ constexpr int U = 4;        // load instructions in flight per wavefront
 }  // namespace dwalk
 
 // GROUPS (variant 60): every wavefront streams its records the per-group way (the product's form).
-template <int MODE, bool NOSTORE, bool GROUPS = false>
+// SEG (variant 61, emit): the 64-B segments that hold a record's fields go out whole from its LDS
+// window, the fields patched in, as the walk kernel's variant 39 does for fixed strides (§5 of
+// a whole segment is a plain write at the memory side, a 2-B store a read-modify-write).
+// SEGF bit 0: whole segments (variant 61); bit 1: the header windows loaded with the default cache
+// policy instead of non-temporal (62 = both, 63 = bit 1 alone, experiments).
+template <int MODE, bool NOSTORE, bool GROUPS = false, int SEGF = 0>
 __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     using namespace dwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
@@ -74,6 +85,8 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     contig = contig && A[cnt - 1] + L[cnt - 1] - span_lo < (1ull << 31);
 
     // ---- the windows: instruction w, lane l: record 4 w + l / 16, chunk l % 16 ----
+    constexpr bool SEG = (SEGF & 1) != 0 && MODE == MODE_EMIT;
+    constexpr bool WNT = (SEGF & 2) == 0;
     const bool mine = (uint32_t)gw < cnt;
     const uint64_t r = rw0 + (uint64_t)gw;
     const uint64_t a0 = (uint64_t)p.buf + ((uint64_t)(uint32_t)__shfl((int)d.x, gw, 64) |
@@ -91,7 +104,7 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
             const uint32_t rl = (uint32_t)__shfl((int)d.z, rec, 64);
             const uint64_t rb = ra & ~127ull;
             const bool in = (uint32_t)rec < cnt && rb + 16ull * (uint32_t)c < ra + rl;
-            wc[w] = ld16<true>((gcv4)(in ? rb + 16ull * (uint32_t)c : dummy));
+            wc[w] = ld16<WNT>((gcv4)(in ? rb + 16ull * (uint32_t)c : dummy));
         }
 #pragma unroll
         for (int w = 0; w < 2; ++w) {
@@ -110,6 +123,33 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     if (mine) g = parse_geometry<false>(rd, len, kind, EMIT);
     const bool l4 = g.proto != P_NONE && !(g.st & SMOL_ST_MALFORMED);
     if (lane == 0) spanbuf[gib] = mine && l4 ? g.span_end : 0u;
+    // SEG: which of the record's field segments go out whole.  A segment that starts before the
+    // record also holds the previous record's last bytes: whole only when that record lies right
+    // before this one in the same wavefront (contig) and has no field in its last 64 bytes (then it
+    // is longer than 64 bytes, and no store of its group falls into the segment).  A record whose
+    // fields end 64 bytes or more before its end keeps its segments inside itself; the window must
+    // hold the whole segment.  The rest are stored as 2-B fields.
+    uint64_t wsA = ~0ull, wsB = ~0ull;
+    if constexpr (SEG) {
+        uint32_t f[3], flo = NO_FIELD, fhi = 0;
+        emit_fields(g, f);
+        for (int j = 0; j < 3; ++j)
+            if (f[j] != NO_FIELD) {
+                flo = f[j] < flo ? f[j] : flo;
+                fhi = f[j] + 2 > fhi ? f[j] + 2 : fhi;
+            }
+        const bool ok_tail = mine && (fhi == 0 || fhi + 64 <= len);
+        const uint64_t okm = __ballot(lane == 0 && ok_tail);
+        if (mine && (g.fam == 4 || g.fam == 6) && fhi != 0 && ok_tail) {
+            const bool prev_ok = contig && gw != 0 && ((okm >> (uint32_t)(G * (gw - 1))) & 1ull);
+            const int32_t ph = (int32_t)(a0 & 63u);
+            const int32_t rA = ((ph + (int32_t)flo) & ~63) - ph, rB = ((ph + (int32_t)fhi - 1) & ~63) - ph;
+            const int32_t wend = 16 * WIN_CH - (int32_t)hd;
+            auto whole = [&](int32_t rel) { return rB <= rA + 64 && rel + 64 <= wend && (rel >= 0 || prev_ok); };
+            if (whole(rA)) wsA = a0 + (int64_t)rA;
+            if (rB != rA && whole(rB)) wsB = a0 + (int64_t)rB;
+        }
+    }
     wave_lds_sync();
     uint32_t S1[R];
 #pragma unroll
@@ -201,12 +241,30 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
         }
     }
     // ---- finish: the walk kernel's gates ----
-    if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane);
+    if constexpr (SEG) {
+        uint8_t* winw = reinterpret_cast<uint8_t*>(&win[gib][0]);
+        if (mine) finish_gates<G, MODE, false, decltype(rd), 16 * WIN_CH, true, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane,
+                                                                                          winw, wsA, wsB);
+        wave_lds_sync();
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        const uint64_t base = a0 & ~127ull;
+        auto seg_store = [&](uint64_t dst) {
+            const u32x2 x = *reinterpret_cast<const u32x2*>(winb + (dst - base));
+            if constexpr (NOSTORE) asm volatile("" ::"v"(x), "v"(dst));
+            else *(GMEM u32x2*)dst = x;
+        };
+        if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
+        if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
+    } else {
+        if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane);
+    }
 }
 
 hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) {
 #ifndef SMOL_EXP
-    if (variant != 60 || mode != MODE_VERIFY) return hipErrorInvalidValue;  // the product's form
+    // the product's forms: 63 (verify / emit), 60 (verify)
+    if (!(variant == 63 && (mode == MODE_VERIFY || mode == MODE_EMIT)) && !(variant == 60 && mode == MODE_VERIFY))
+        return hipErrorInvalidValue;
 #endif
     const uint64_t per = (uint64_t)dwalk::GPB;
     note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
@@ -217,10 +275,17 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         q.desc = p.desc + i0;
         if (p.status) q.status = p.status + i0;
         const uint32_t b = grid_blocks((q.n + per - 1) / per, kMaxGridBlocks);
-        if (variant == 60 && mode == MODE_VERIFY)
+        if (variant == 63 && mode == MODE_VERIFY)
+            hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false, true, 2>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 63)
+            hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 2>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 60 && mode == MODE_VERIFY)
             hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false, true>), dim3(b), dim3(256), 0, s, q);
 #ifdef SMOL_EXP
         else if (variant == 60) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 61) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 1>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 62) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 3>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 64 + 61) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, true, true, 1>), dim3(b), dim3(256), 0, s, q);
         else if (mode == MODE_VERIFY) hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false>), dim3(b), dim3(256), 0, s, q);
         else if (variant >= 64) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, true>), dim3(b), dim3(256), 0, s, q);
         else hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false>), dim3(b), dim3(256), 0, s, q);

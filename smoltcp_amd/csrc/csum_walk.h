@@ -71,21 +71,25 @@ struct VarT {
     // 37 / 38: variant 5 with whole field segments decided by one ballot (BSEG; 38 also IPv6 records)
     // 39: variant 29 on a wavefront that holds an IPv4 record, 38's ballot decision on one that holds
     // none (BSEG_NO4: IPv6 records get whole segments too)
-    static constexpr bool BSEG = VAR == 37 || VAR == 38 || VAR == 39 || VAR == 40;
-    static constexpr bool BSEG6 = VAR == 38 || VAR == 39 || VAR == 40;
-    static constexpr bool BSEG_NO4 = VAR == 39 || VAR == 40;
+    // 12 / 14 (experiments build): 39 with the header lines (chunks u < 2 of a step: the LDS window)
+    // loaded with the default cache policy, at a group's first load only (12) or at every step (14),
+    // so that the field stores hit lines the L2 holds
+    static constexpr bool BSEG = VAR == 37 || VAR == 38 || VAR == 39 || VAR == 40 || VAR == 12 || VAR == 14;
+    static constexpr bool BSEG6 = VAR == 38 || VAR == 39 || VAR == 40 || VAR == 12 || VAR == 14;
+    static constexpr bool BSEG_NO4 = VAR == 39 || VAR == 40 || VAR == 12 || VAR == 14;
+    static constexpr int CU0 = VAR == 12 ? 2 : 0;
     // 40 (experiments build): 39 with the whole segments stored non-temporal
     static constexpr bool NTSEG = VAR == 40;
     static constexpr bool NOSHARE = VAR == 31 || VAR == 32 || VAR == 34 || VAR == 35;
     static constexpr int BASE = (VAR == 31 || VAR == 35 || VAR == 36 || VAR == 37 || VAR == 38) ? 5
-                                : ((VAR >= 32 && VAR <= 34) || VAR == 39 || VAR == 40) ? 29 : VAR;
+                                : ((VAR >= 32 && VAR <= 34) || VAR == 39 || VAR == 40 || VAR == 12 || VAR == 14) ? 29 : VAR;
     static constexpr bool NT = VAR == 0 || VAR == 2 || VAR == 5 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                               (VAR >= 23 && VAR <= 29) || (VAR >= 31 && VAR <= 40);
+                               (VAR >= 23 && VAR <= 29) || (VAR >= 31 && VAR <= 40) || VAR == 12 || VAR == 14;
     static constexpr bool PF = VAR != 2 && VAR != 8 && VAR != 11 && VAR != 13 && VAR != 16 && VAR != 26 && VAR != 27 &&
                                VAR != 28;
     static constexpr bool LINE = VAR == 5 || VAR == 6 || VAR == 9 || VAR == 10 || VAR == 13 || VAR == 19 ||
-                                 (VAR >= 23 && VAR <= 29) || (VAR >= 31 && VAR <= 40);
-    static constexpr int CACHED_U = VAR == 9 ? 2 : VAR == 10 ? 1 : 0;
+                                 (VAR >= 23 && VAR <= 29) || (VAR >= 31 && VAR <= 40) || VAR == 12 || VAR == 14;
+    static constexpr int CACHED_U = (VAR == 9 || VAR == 14) ? 2 : VAR == 10 ? 1 : 0;
     static constexpr bool SHUF = VAR == 11 || VAR == 16;
     static constexpr bool WHOLE = VAR == 16;
     static constexpr bool SHUF2 = VAR == 16;
@@ -1197,7 +1201,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MinWaves<VA
     Regs<U, COPY> va;
     if (PF) {
         Regs<U, COPY> vb;
-        load_step<G, U, NT, COPY, LINE, CU, SHUF>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
+        load_step<G, U, NT, COPY, LINE, (VarT<VAR>::CU0 ? VarT<VAR>::CU0 : CU), SHUF>(va, w.cur, w.nch, 0, lane, true, (uint64_t)p.dummy,
                                                   shared_from<G, MODE, IMPLICIT, LINE, VarT<VAR>::NOSHARE>(p, w.r, w.cur.a0, gib, ngroups));
         // the body is instantiated twice with the register sets' roles swapped
         while (true) {
@@ -1285,6 +1289,8 @@ hipError_t launch_walk_exp(int shape, int var, const KParams& p, uint32_t max_bl
             case 37: return launch_emit_exp<37>(shape, p, max_blocks, s);
             case 38: return launch_emit_exp<38>(shape, p, max_blocks, s);
             case 40: return launch_emit_exp<40>(shape, p, max_blocks, s);
+            case 12: return launch_emit_exp<12>(shape, p, max_blocks, s);
+            case 14: return launch_emit_exp<14>(shape, p, max_blocks, s);
             case 64 + 39: return launch_emit_exp<64 + 39>(shape, p, max_blocks, s);
             case 64 + 5: return launch_emit_exp<64 + 5>(shape, p, max_blocks, s);
             case 64 + 29: return launch_emit_exp<64 + 29>(shape, p, max_blocks, s);
@@ -1333,7 +1339,7 @@ hipError_t launch_walk_exp(int shape, int var, const KParams& p, uint32_t max_bl
             }
             return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);
         case 0: return launch_shape<MODE, IMPLICIT, 0>(shape, p, max_blocks, s);
-        case 31: case 32: case 33: case 34: case 35: case 36: case 37: case 38: case 40:
+        case 31: case 32: case 33: case 34: case 35: case 36: case 37: case 38: case 40: case 12: case 14:
             return launch_shape<MODE, IMPLICIT, 5>(shape, p, max_blocks, s);  // emit variants: 5 elsewhere
         default: return hipErrorInvalidValue;
     }

@@ -63,14 +63,17 @@ def _run_records(eng, records, kinds, caps=CAPS_DEFAULT, gap_seed=None, shape=-1
         assert bad.size == 0, f"verify mismatch at {bad[:8]}: got {st[bad[:8]]} want {ref_st[bad[:8]]}"
         est = torch.zeros(len(records), dtype=torch.uint8, device="cuda:0")
         eng.emit(d, batch, caps=caps, status=est)
+        launched_e = eng.last_launch()
         got = d.cpu().numpy()
         ref = buf.copy()
         ref_est = P.oracle_emit_records(ref, offs, lens, kinds, caps)
         diff = np.nonzero(got != ref)[0]
         assert diff.size == 0, f"emit bytes differ at {diff[:8]}"
         assert np.array_equal(est.cpu().numpy(), ref_est), "emit status differs"
-        if variant in (56, 60) and len(records):  # verify ran the descriptor walk it names
+        if variant in (56, 60, 63) and len(records):  # verify ran the descriptor walk it names
             assert (launched_v["kernel"], launched_v["variant"]) == ("dwalk_kernel", variant), launched_v
+        if variant in (61, 62, 63) and len(records):  # so did emit
+            assert (launched_e["kernel"], launched_e["variant"]) == ("dwalk_kernel", variant), launched_e
         return st, got, offs, lens
     finally:
         eng.set_shape(-1)
@@ -279,10 +282,12 @@ def _mixed_records(rng, n=240):
     return recs
 
 
-@pytest.mark.parametrize("variant", [56, 60])
+@pytest.mark.parametrize("variant", [56, 60, 61, 62, 63])
 def test_dwalk_descriptor_batches(eng, variant):
-    """The transposed walk over descriptor batches (variant 56, experiments build): packed records
-    (one wave-contiguous span per 8 records), gapped and shuffled descriptors (one span per record),
+    """The descriptor walks (63: the product's descriptor verify / emit, cached header windows; 60:
+    non-temporal windows; experiments build: 56, and 61 / 62 = 60's / 63's emit with whole field
+    segments): packed records (one wave-contiguous span per 8 records; segments reaching
+    into the previous record), gapped and shuffled descriptors (one span per record),
     tiny and empty records, records of 20-60 KB, Ethernet / raw / malformed records, every caps
     gate; verify statuses and emitted bytes against the oracle."""
     eng.need(variant)
@@ -673,7 +678,7 @@ def _expected_launch(variant, op, has_desc):
     if variant in (3, 4, 7):
         return ("csum_tile_kernel", {3: 0, 4: 1, 7: 2}[variant])
     emit_fixed = op == "emit" and not has_desc
-    if variant in (9, 10, 29, 37, 38, 39):
+    if variant in (9, 10, 12, 14, 29, 37, 38, 39):
         return ("csum_kernel", variant if emit_fixed else 5)
     if 23 <= variant <= 28:
         if op == "emit":
@@ -682,7 +687,7 @@ def _expected_launch(variant, op, has_desc):
     return ("csum_kernel", variant)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 13, 19, 23, 24, 25, 26, 27, 28, 29, 37, 38, 39])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 12, 13, 14, 19, 23, 24, 25, 26, 27, 28, 29, 37, 38, 39])
 def test_variants_fixed_stride(eng, variant):
     """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
     the oracle on fixed-stride batches: strides equal to the record length (neighbours share

@@ -232,7 +232,8 @@ def test_emit_write_set_concurrent(eng, gap, L):
     s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
     K = 120
     for variant, batch in ((19, fixed), (29, fixed), (-1, fixed), (23, fixed), (26, desc_batch), (28, desc_batch),
-                           (-1, desc_batch), (37, fixed), (39, fixed), (44, fixed), (47, fixed)):
+                           (-1, desc_batch), (37, fixed), (39, fixed), (44, fixed), (47, fixed), (12, fixed),
+                           (61, desc_batch), (62, desc_batch)):
         if not eng.has(variant):
             continue
         d = torch.from_numpy(host0.copy()).cuda()
@@ -267,7 +268,7 @@ def test_field_stores_flag(eng):
     ref = host.copy()
     oracle.batch_emit(ref, desc, n)
     batch = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0", batch_flags=E.BATCH_FIELD_STORES)
-    for variant in eng.avail((-1, 19, 23, 26, 27, 28, 29, 39, 7)):
+    for variant in eng.avail((-1, 19, 23, 26, 27, 28, 29, 39, 7, 61, 62)):
         d = torch.from_numpy(host.copy()).cuda()
         eng.set_variant(variant)
         try:

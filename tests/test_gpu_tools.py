@@ -89,13 +89,21 @@ def test_last_launch_families(eng):
         assert want[2] is None or ll["G"] == want[2], (LL, stride, op, ll)
     offs = np.arange(n, dtype=np.uint64) * L
     bd = E.Batch.from_records(offs, np.full(n, L, np.uint32), E.KIND_IP, "cuda:0")
+    # descriptor batches: the per-group descriptor walk (csum_dwalk.hip, cached header windows),
+    # 8 lanes x 4 chunks, both operations; the tile kernel when forced (variant 7)
     eng.emit(buf, bd)
     ll = eng.last_launch()
-    assert (ll["kernel"], ll["variant"]) == ("csum_tile_kernel", 2), ll
+    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 63, 8, 4), ll
     eng.verify(buf, bd)
     ll = eng.last_launch()
-    # descriptor-batch verify: the per-group descriptor walk (csum_dwalk.hip), 8 lanes x 4 chunks
-    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 60, 8, 4), ll
+    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 63, 8, 4), ll
+    eng.set_variant(7)
+    try:
+        eng.emit(buf, bd)
+        ll = eng.last_launch()
+    finally:
+        eng.set_variant(-1)
+    assert (ll["kernel"], ll["variant"]) == ("csum_tile_kernel", 2), ll
     src = torch.zeros(n * 1472 + 16, dtype=torch.uint8, device="cuda:0")
     cp = torch.from_numpy(E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472).view(np.uint8).copy()).cuda()
     eng.copy_emit(buf, b, src, cp)
