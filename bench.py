@@ -60,6 +60,8 @@ def parse_args(argv=None):
                     help="CPU-baseline budget, split between 1 thread and all threads (0: skip)")
     ap.add_argument("--shape", type=int, default=-1, help="force a launch shape (tuning)")
     ap.add_argument("--variant", type=int, default=-1, help="force a kernel variant (tuning)")
+    ap.add_argument("--emit-variant", type=int, default=-1, help="force a kernel variant for emit only (tuning)")
+    ap.add_argument("--verify-variant", type=int, default=-1, help="force a kernel variant for verify only (tuning)")
     ap.add_argument("--xcd-remap", type=int, default=-1, help="1/0: force the XCD-contiguous block order (tuning; "
                                                                "-1: the library's choice)")
     ap.add_argument("--launch-records", type=int, default=-1, help="records per kernel launch (tuning; 0: all)")
@@ -613,6 +615,7 @@ def main(argv=None):
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
+    split_variants = args.emit_variant >= 0 or args.verify_variant >= 0  # (set per operation, host-side)
     R = len(wl.txs)
     nstep = [0]
     launched = {}  # the kernel each op ran (smol_csum_tool_last_launch), recorded at instrumented steps
@@ -623,6 +626,8 @@ def main(argv=None):
         nstep[0] += 1
         if ev is not None:
             ev[0].record(stream)
+        if split_variants:
+            eng.set_variant(args.emit_variant if args.emit_variant >= 0 else args.variant)
         if wl.copy is not None:
             eng.copy_emit(wl.txs[j], wl.batch, wl.src, wl.copy, stream=stream)
         else:
@@ -630,6 +635,8 @@ def main(argv=None):
         if ev is not None:
             launched["copy_emit" if wl.copy is not None else "emit"] = eng.last_launch()
             ev[1].record(stream)
+        if split_variants:
+            eng.set_variant(args.verify_variant if args.verify_variant >= 0 else args.variant)
         eng.verify(wl.rxs[j], wl.batch, status=wl.status, stream=stream)
         if ev is not None:
             launched["verify"] = eng.last_launch()

@@ -129,11 +129,21 @@ int auto_variant(int mode, bool has_desc) {
 // (12000), emit within 2 % of that.  The walk kernel's shapes leave lanes idle from 1666 B (8 x 7
 // x 2 chunks no longer hold a record) and fit whole 128-B lines exactly at multiples of 128 B; past
 // 8065 B the transposed walk takes one record per wavefront and the two trade places by length.
-bool xwalk_auto(int mode, const smol_csum_batch_t* b) {
-    if (b->desc || b->stride < b->len || (mode != MODE_VERIFY && mode != MODE_EMIT)) return false;
+//
+// Variant 45 (47 with each record's first KiB loaded with the default cache policy, so that emit's
+// field stores hit lines the L2 holds) for emit of packed 1400-1580-B records, not multiples of 64 B.
+// Emit in bench.py's step order (emit of TX batch i, then the default verify of RX batch i, R = 4;
+// tools/exp_r05_vlen.py STEP=1, profiles/r05_experiments/xwalk_cached_first_kib.txt), walk 39 / 45,
+// ms: IPv4/UDP 1400 0.333 / 0.320, 1500 0.328 / 0.320, 1580 0.320 / 0.316, 1600 0.291 / 0.310,
+// 1650 0.313 / 0.315; C2 in bench.py 0.3214 -> 0.3124 ms (5318 -> 5400 GiB/s).  C4's IPv6 mix at
+// 1320 B lost 1 % with it (outside the range), at 1500 B 1.7 %.
+// Returns the transposed-walk variant to run (0: none).
+int xwalk_auto(int mode, const smol_csum_batch_t* b) {
+    if (b->desc || b->stride < b->len || (mode != MODE_VERIFY && mode != MODE_EMIT)) return 0;
     const bool packed = b->stride == b->len;
-    if (b->len >= 1666) return b->len <= 8065;
-    return mode == MODE_VERIFY && packed && b->len >= 1473 && b->len % 128 != 0;
+    if (b->len >= 1666) return b->len <= 8065 ? 47 : 0;
+    if (mode == MODE_EMIT) return packed && b->len >= 1400 && b->len <= 1580 && b->len % 64 != 0 ? 45 : 0;
+    return packed && b->len >= 1473 && b->len % 128 != 0 ? 47 : 0;
 }
 
 // The XCD block order (csum_launch.h xcd_block / xcd_chunk) when none is forced: the contiguous order
@@ -156,7 +166,7 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
-    if (variant == 47) return 44;
+    if (variant == 47 || variant == 45) return 44;
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62) return 63;  // (63 stores 2-B fields only)
     if (variant == 26 || variant == 27 || variant == 28) return 13;
@@ -169,14 +179,14 @@ int field_store_variant(int variant, bool has_desc) {
 // field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
 bool variant_built(int v) {
     switch (v) {
-        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 47: case 60: case 63: return true;
+        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 45: case 47: case 60: case 63: return true;
         default: break;
     }
 #ifdef SMOL_EXP
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
+           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
 #else
     return false;
 #endif
@@ -251,7 +261,10 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     // run variant 0 for it).
     int variant = ctx->variant;
     const bool has_desc = b->desc != nullptr;
-    if (variant < 0) variant = (!d_addrs && xwalk_auto(mode, b)) ? 47 : auto_variant(mode, has_desc);
+    if (variant < 0) {
+        const int xv = d_addrs ? 0 : xwalk_auto(mode, b);
+        variant = xv ? xv : auto_variant(mode, has_desc);
+    }
     if (mode == MODE_EMIT && (b->flags & SMOL_BATCH_FIELD_STORES)) variant = field_store_variant(variant, has_desc);
     // the stripe kernel (variant 42) serves emit / verify of packed fixed-stride records of 1024-1520 B
     // a kernel that does not serve the batch falls back to the default of its kind (descriptor emit:
@@ -260,7 +273,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
     if (variant == 42 && !stripe) variant = fallback;
     // the transposed walk (variants 44 / 47, 64 + 44 / 47): fixed-stride records of 1024 - 16257 B
-    const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 48 || variant == 57 || variant == 58 || variant == 59;
+    const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 43 || variant == 45 || variant == 48 || variant == 57 ||
+                        variant == 58 || variant == 59;
     const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
     if (xw_var && !xwalk) variant = fallback;
     // descriptor-batch walks: 63 = verify / emit default (cached header windows), 60 = its
@@ -270,7 +284,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63;
     if (variant % 64 == 61 && mode == MODE_VERIFY) variant = 60;  // an emit form of 60
     if (variant == 62 && mode == MODE_VERIFY) variant = 63;      // an emit form of 63
-    const bool dwalk = dw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && has_desc && !d_addrs;
+    // (forced, the experiments build also runs it over fixed-stride batches)
+    const bool dwalk = dw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs;
 #else
     const bool dw_var = variant == 60 || variant == 63;
     const bool dwalk = dw_var && (mode == MODE_VERIFY || (mode == MODE_EMIT && variant == 63)) && has_desc && !d_addrs;

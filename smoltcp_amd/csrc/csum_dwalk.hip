@@ -66,7 +66,14 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     const uint64_t dummy = (uint64_t)p.dummy;
 
     // ---- descriptors: lane j holds record j's ----
-    const u32x4 d = (uint32_t)wl < cnt ? *(gcv4)((uint64_t)p.desc + 16 * (rw0 + (uint64_t)wl)) : u32x4{0, 0, 0, 0};
+    // (a fixed-stride batch, experiments build: the descriptors it implies)
+    u32x4 d = u32x4{0, 0, 0, 0};
+    if (p.desc) {
+        if ((uint32_t)wl < cnt) d = *(gcv4)((uint64_t)p.desc + 16 * (rw0 + (uint64_t)wl));
+    } else {
+        const uint64_t off = (rw0 + (uint64_t)wl) * p.stride;
+        d = u32x4{(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)wl < cnt ? p.len : 0u, 0u};
+    }
     // wave-uniform record extents
     uint64_t A[R];
     uint32_t L[R];
@@ -92,7 +99,7 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     const uint64_t a0 = (uint64_t)p.buf + ((uint64_t)(uint32_t)__shfl((int)d.x, gw, 64) |
                                            ((uint64_t)(uint32_t)__shfl((int)d.y, gw, 64) << 32));
     const uint32_t len = (uint32_t)__shfl((int)d.z, gw, 64);
-    const uint32_t kind = desc_kind((uint32_t)__shfl((int)d.w, gw, 64));
+    const uint32_t kind = p.desc ? desc_kind((uint32_t)__shfl((int)d.w, gw, 64)) : p.kind;
     const uint32_t hd = (uint32_t)(a0 & 127u);
     {
         u32x4 wc[2];
@@ -272,7 +279,8 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
     for (uint64_t i0 = 0; i0 < p.n; i0 += span) {
         KParams q = p;
         q.n = p.n - i0 < span ? p.n - i0 : span;
-        q.desc = p.desc + i0;
+        if (p.desc) q.desc = p.desc + i0;
+        else q.buf = p.buf + i0 * p.stride;
         if (p.status) q.status = p.status + i0;
         const uint32_t b = grid_blocks((q.n + per - 1) / per, kMaxGridBlocks);
         if (variant == 63 && mode == MODE_VERIFY)

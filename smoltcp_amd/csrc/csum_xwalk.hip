@@ -75,7 +75,11 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // over the batch, issuing the next step's loads as soon as this step's sums are taken (before its
 // finish and stores), so that no wavefront ends while its stores drain.
 // NTS (experiments build): the segments stored non-temporal, always (variant 57) or on a wavefront
-// that holds an IPv4 record (58).
+// that holds an IPv4 record (58).  NTS = 4 (variant 45, the product's emit of packed 1400-1580-B
+// records, csum_api.cpp xwalk_auto): each record's first load instruction (its first KiB, header
+// lines included) with the default cache policy instead of non-temporal, so that the field stores
+// hit lines the L2 holds (the descriptor walk's variant 63 finding).  NTS = 8 (variant 43,
+// experiments build): every load with the default cache policy.
 // HALF (variant 59, experiments build; R = 8, records of at most 1409 B, whose line-grid span fits
 // 96 chunks): a record's second KiB is half an instruction, two records per instruction, so a
 // wavefront issues 12 loads instead of 16.
@@ -128,7 +132,9 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
 #pragma unroll
             for (int s = 0; s < (HALF ? 1 : NS); ++s) {
                 const uint32_t k = (uint32_t)(64 * s + wl);
-                v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, k < nload[j] ? 16u * k : 0x80000000u, soff, 2 /* nt */);
+                const uint32_t o = k < nload[j] ? 16u * k : 0x80000000u;
+                if ((NTS == 4 && s == 0) || NTS == 8) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
+                else v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 2 /* nt */);
             }
         }
         if constexpr (HALF) {
@@ -313,6 +319,11 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
             return;
         }
     }
+    if (variant == 43) {
+        if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 8>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 8>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
     if (variant == 57 || variant == 58) {
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
         else if (variant == 57) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
@@ -331,8 +342,8 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #endif
-    const bool seg = variant % 64 == 47;
-    if (mode == MODE_VERIFY) {
+    const bool seg = variant % 64 == 47 || variant == 45;
+    if (mode == MODE_VERIFY) {  // (45: 47's verify; its cached first KiB measured slower there)
         hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
@@ -343,7 +354,8 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #endif
-    if (seg) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true>), dim3(blocks), dim3(256), 0, s, p);
+    if (variant == 45) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 4>), dim3(blocks), dim3(256), 0, s, p);
+    else if (seg) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true>), dim3(blocks), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
 }
 

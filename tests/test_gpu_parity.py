@@ -680,6 +680,8 @@ def _expected_launch(variant, op, has_desc):
     emit_fixed = op == "emit" and not has_desc
     if variant in (9, 10, 12, 14, 29, 37, 38, 39):
         return ("csum_kernel", variant if emit_fixed else 5)
+    if variant == 62:  # the descriptor walk over fixed strides (experiments build; verify: 63)
+        return ("dwalk_kernel", 62 if op == "emit" else 63)
     if 23 <= variant <= 28:
         if op == "emit":
             return ("csum_kernel", variant)
@@ -687,7 +689,8 @@ def _expected_launch(variant, op, has_desc):
     return ("csum_kernel", variant)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 12, 13, 14, 19, 23, 24, 25, 26, 27, 28, 29, 37, 38, 39])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 12, 13, 14, 19, 23, 24, 25, 26, 27, 28, 29, 37, 38,
+                                     39, 62])
 def test_variants_fixed_stride(eng, variant):
     """The non-default kernel variants (walk: nt + prefetch, nt only; tile: nt, plain loads) against
     the oracle on fixed-stride batches: strides equal to the record length (neighbours share
@@ -735,6 +738,7 @@ WIDE_KERNELS = {
     # variant: (kernel name, the largest record length it serves)
     42: ("csum_tile_kernel", 1520),
     44: ("xwalk_kernel", 16257),
+    45: ("xwalk_kernel", 16257),
     47: ("xwalk_kernel", 16257),
     48: ("xwalk_kernel", 16257),
     59: ("xwalk_kernel", 16257),

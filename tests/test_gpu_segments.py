@@ -277,10 +277,10 @@ def test_field_stores_flag(eng):
         finally:
             eng.set_variant(-1)
         assert np.array_equal(got, ref), (variant, np.nonzero(got != ref)[0][:8])
-    # fixed-stride C2-like batches (1500 B: the walk kernel; 2500 B: the transposed walk): UDP
+    # fixed-stride C2-like batches (1500 B, 2500 B: the transposed walk; 1600 B: the walk kernel): UDP
     # payload bytes 30..63 of every record (in the segment that holds the IPv4 header and UDP
     # checksums) rewritten from another stream while emit runs
-    for n, L in ((1 << 15, 1500), (1 << 14, 2500)):
+    for n, L in ((1 << 15, 1500), (1 << 14, 2500), (1 << 15, 1600)):
         buf = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
         fixed = E.Batch.fixed(n, L, L, E.KIND_IP, flags=E.BATCH_FIELD_STORES)
         eng.synth(buf, fixed, E.SYNTH_UDP4, seed=5)
@@ -295,4 +295,5 @@ def test_field_stores_flag(eng):
                 eng.emit(buf, fixed, stream=s_emit)
         torch.cuda.synchronize()
         assert bool((payload == K).all()), L
-        assert eng.last_launch()["kernel"] == ("xwalk_kernel" if L == 2500 else "csum_kernel")
+        ll = eng.last_launch()
+        assert (ll["kernel"], ll["variant"]) == (("csum_kernel", 5) if L == 1600 else ("xwalk_kernel", 44)), (L, ll)

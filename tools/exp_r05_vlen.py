@@ -4,6 +4,9 @@ transposed walk (variants 44 / 47) over record lengths, ~1.5 GB per batch, R = 4
 (synthetic IPv4/UDP, every 64th record corrupted; emit timed after verify on the same batches).
 Needs the experiments build (SMOLCSUM_LIB=.../libsmolcsum_exp.so).
 GAP=g: stride = length + g (default 0, packed).
+STEP=1: emit timed as in bench.py's step instead: emit of TX batch i mod R (its own buffers, HIP
+events around each emit), then the default verify of RX batch i mod R.
+PROFILE=v6mix: the IPv6 TCP / UDP / ICMPv6 mix (C4's) instead of IPv4/UDP.
 Usage: [LENS=1024,1320,1500] [VVARS=-1,44] [EVARS=-1,44,47] [GAP=0] [K=24] exp_r05_vlen.py"""
 import json
 import os
@@ -30,7 +33,8 @@ def main():
         rxs = []
         for j in range(R):
             b = torch.empty(n * S + 64, dtype=torch.uint8, device="cuda:0")
-            eng.synth(b, batch, E.SYNTH_UDP4, seed=L + j)
+            prof = E.SYNTH_V6MIX if os.environ.get("PROFILE") == "v6mix" else E.SYNTH_UDP4
+            eng.synth(b, batch, prof, seed=L + j)
             eng.emit(b, batch)
             eng.corrupt(b, batch, every=64, seed=j)
             rxs.append(b)
@@ -52,8 +56,30 @@ def main():
             torch.cuda.synchronize()
             return a.elapsed_time(b) / K
 
+        txs = [b.clone() for b in rxs] if os.environ.get("STEP") else None
+
+        def step_emit(v):
+            ev_ = []
+            for i in range(K + R):
+                j = i % R
+                eng.set_variant(v)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                eng.emit(txs[j], batch)
+                b.record()
+                eng.set_variant(-1)
+                eng.verify(rxs[j], batch, status=st)
+                if i >= R:
+                    ev_.append((a, b))
+            torch.cuda.synchronize()
+            return sum(a.elapsed_time(b) for a, b in ev_) / len(ev_)
+
         res = {}
         for rnd in range(3):
+            if txs is not None:
+                for v in ev:
+                    res.setdefault(f"step_emit{v}", []).append(step_emit(v))
+                continue
             for v in vv:
                 eng.set_variant(v)
                 res.setdefault(f"verify{v}", []).append(timed(lambda j: eng.verify(rxs[j], batch, status=st)))
