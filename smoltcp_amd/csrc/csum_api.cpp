@@ -186,7 +186,7 @@ bool variant_built(int v) {
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
+           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 46 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
 #else
     return false;
 #endif
@@ -273,7 +273,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
     if (variant == 42 && !stripe) variant = fallback;
     // the transposed walk (variants 44 / 47, 64 + 44 / 47): fixed-stride records of 1024 - 16257 B
-    const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 43 || variant == 45 || variant == 48 || variant == 57 ||
+    const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 43 || variant == 45 || variant == 46 ||
+                        variant == 48 || variant == 57 ||
                         variant == 58 || variant == 59;
     const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
     if (xw_var && !xwalk) variant = fallback;

@@ -79,7 +79,8 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // records, csum_api.cpp xwalk_auto): each record's first load instruction (its first KiB, header
 // lines included) with the default cache policy instead of non-temporal, so that the field stores
 // hit lines the L2 holds (the descriptor walk's variant 63 finding).  NTS = 8 (variant 43,
-// experiments build): every load with the default cache policy.
+// experiments build): every load with the default cache policy; NTS = 16 (variant 46, experiments
+// build): only the record's two header lines (lanes 0-15 of its first instruction) cached.
 // HALF (variant 59, experiments build; R = 8, records of at most 1409 B, whose line-grid span fits
 // 96 chunks): a record's second KiB is half an instruction, two records per instruction, so a
 // wavefront issues 12 loads instead of 16.
@@ -134,7 +135,10 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
                 const uint32_t k = (uint32_t)(64 * s + wl);
                 const uint32_t o = k < nload[j] ? 16u * k : 0x80000000u;
                 if ((NTS == 4 && s == 0) || NTS == 8) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
-                else v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 2 /* nt */);
+                else if (NTS == 16 && s == 0) {  // the header lines cached, the rest of the KiB nt
+                    if (wl < 16) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
+                    else v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 2);
+                } else v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 2 /* nt */);
             }
         }
         if constexpr (HALF) {
@@ -318,6 +322,11 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
             else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, 8, false, true, false, 0, true>), dim3(blocks), dim3(256), 0, s, p);
             return;
         }
+    }
+    if (variant == 46) {
+        if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 16>), dim3(blocks), dim3(256), 0, s, p);
+        return;
     }
     if (variant == 43) {
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 8>), dim3(blocks), dim3(256), 0, s, p);
