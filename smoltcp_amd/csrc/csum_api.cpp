@@ -130,19 +130,20 @@ int auto_variant(int mode, bool has_desc) {
 // x 2 chunks no longer hold a record) and fit whole 128-B lines exactly at multiples of 128 B; past
 // 8065 B the transposed walk takes one record per wavefront and the two trade places by length.
 //
-// Variant 45 (47 with each record's first KiB loaded with the default cache policy, so that emit's
-// field stores hit lines the L2 holds) for emit of packed 1400-1580-B records, not multiples of 64 B.
-// Emit in bench.py's step order (emit of TX batch i, then the default verify of RX batch i, R = 4;
-// tools/exp_r05_vlen.py STEP=1, profiles/r05_experiments/xwalk_cached_first_kib.txt), walk 39 / 45,
-// ms: IPv4/UDP 1400 0.333 / 0.320, 1500 0.328 / 0.320, 1580 0.320 / 0.316, 1600 0.291 / 0.310,
-// 1650 0.313 / 0.315; C2 in bench.py 0.3214 -> 0.3124 ms (5318 -> 5400 GiB/s).  C4's IPv6 mix at
-// 1320 B lost 1 % with it (outside the range), at 1500 B 1.7 %.
+// Variant 57 (47 with the field segments stored non-temporal) for emit of packed 1400-1580-B
+// records, not multiples of 64 B.  Emit in bench.py's step order (emit of TX batch i, then the
+// default verify of RX batch i, R = 4; tools/exp_r05_vlen.py STEP=1,
+// profiles/r05_experiments/xwalk_cached_first_kib.txt, xwalk_nt_segments_step.txt), walk 39 / 45
+// (47 with each record's first KiB loaded cached) / 57, ms: IPv4/UDP 1400 0.319 / 0.319 / 0.315,
+// 1500 0.319 / 0.320 / 0.316, 1536 0.291 / 0.291 / 0.309, 1600 0.290 / 0.310 / 0.313; C2 in bench.py
+// 0.3214 (39) -> 0.3124 (45) -> 0.3084 ms (57), 5318 -> 5400 -> 5449 GiB/s.  C4's IPv6 mix at 1320 B
+// (outside the range): 57 0.273 against walk 39's 0.271 ms; 45 lost 1.7 % on it at 1500 B.
 // Returns the transposed-walk variant to run (0: none).
 int xwalk_auto(int mode, const smol_csum_batch_t* b) {
     if (b->desc || b->stride < b->len || (mode != MODE_VERIFY && mode != MODE_EMIT)) return 0;
     const bool packed = b->stride == b->len;
     if (b->len >= 1666) return b->len <= 8065 ? 47 : 0;
-    if (mode == MODE_EMIT) return packed && b->len >= 1400 && b->len <= 1580 && b->len % 64 != 0 ? 45 : 0;
+    if (mode == MODE_EMIT) return packed && b->len >= 1400 && b->len <= 1580 && b->len % 64 != 0 ? 57 : 0;
     return packed && b->len >= 1473 && b->len % 128 != 0 ? 47 : 0;
 }
 
@@ -166,7 +167,7 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
-    if (variant == 47 || variant == 45) return 44;
+    if (variant == 47 || variant == 57 || variant == 45) return 44;
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62) return 63;  // (63 stores 2-B fields only)
     if (variant == 26 || variant == 27 || variant == 28) return 13;
@@ -179,14 +180,14 @@ int field_store_variant(int variant, bool has_desc) {
 // field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
 bool variant_built(int v) {
     switch (v) {
-        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 45: case 47: case 60: case 63: return true;
+        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 47: case 57: case 60: case 63: return true;
         default: break;
     }
 #ifdef SMOL_EXP
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 46 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
+           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 45 || v == 46 || v == 15 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
 #else
     return false;
 #endif
@@ -273,7 +274,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
     if (variant == 42 && !stripe) variant = fallback;
     // the transposed walk (variants 44 / 47, 64 + 44 / 47): fixed-stride records of 1024 - 16257 B
-    const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 43 || variant == 45 || variant == 46 ||
+    const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 43 || variant == 45 || variant == 46 || variant == 15 ||
                         variant == 48 || variant == 57 ||
                         variant == 58 || variant == 59;
     const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);

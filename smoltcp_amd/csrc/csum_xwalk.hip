@@ -74,13 +74,15 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // PERSIST (variant 48, experiments build): a grid of the resident workgroups whose wavefronts step
 // over the batch, issuing the next step's loads as soon as this step's sums are taken (before its
 // finish and stores), so that no wavefront ends while its stores drain.
-// NTS (experiments build): the segments stored non-temporal, always (variant 57) or on a wavefront
-// that holds an IPv4 record (58).  NTS = 4 (variant 45, the product's emit of packed 1400-1580-B
-// records, csum_api.cpp xwalk_auto): each record's first load instruction (its first KiB, header
-// lines included) with the default cache policy instead of non-temporal, so that the field stores
-// hit lines the L2 holds (the descriptor walk's variant 63 finding).  NTS = 8 (variant 43,
+// NTS: the segments stored non-temporal, always (variant 57, the product's emit of packed
+// 1400-1580-B records, csum_api.cpp xwalk_auto) or on a wavefront that holds an IPv4 record (58,
+// experiments build).  NTS = 4 (variant 45, experiments build): each record's first load
+// instruction (its first KiB, header lines included) with the default cache policy instead of
+// non-temporal, so that the field stores hit lines the L2 holds (the descriptor walk's variant 63
+// finding).  NTS = 8 (variant 43,
 // experiments build): every load with the default cache policy; NTS = 16 (variant 46, experiments
-// build): only the record's two header lines (lanes 0-15 of its first instruction) cached.
+// build): only the record's two header lines (lanes 0-15 of its first instruction) cached; NTS = 5
+// (variant 15, experiments build): 45 with the segments stored non-temporal.
 // HALF (variant 59, experiments build; R = 8, records of at most 1409 B, whose line-grid span fits
 // 96 chunks): a record's second KiB is half an instruction, two records per instruction, so a
 // wavefront issues 12 loads instead of 16.
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
             for (int s = 0; s < (HALF ? 1 : NS); ++s) {
                 const uint32_t k = (uint32_t)(64 * s + wl);
                 const uint32_t o = k < nload[j] ? 16u * k : 0x80000000u;
-                if ((NTS == 4 && s == 0) || NTS == 8) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
+                if (((NTS == 4 || NTS == 5) && s == 0) || NTS == 8) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
                 else if (NTS == 16 && s == 0) {  // the header lines cached, the rest of the KiB nt
                     if (wl < 16) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
                     else v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 2);
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
         if (mine)
             finish_gates<G, MODE, false, decltype(rd), 16 * WIN_CH, true, NOSTORE>(
                 p, g, lane == 0 ? tot : 0u, rd, winb, hd, a0, r, lane, winw, wsA, wsB);
-        const bool nts = NTS == 1 || (NTS == 2 && __any(mine && g.fam == 4));
+        const bool nts = NTS == 1 || NTS == 5 || (NTS == 2 && __any(mine && g.fam == 4));
         wave_lds_sync();
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
         const uint64_t wb = a0 & ~127ull;
@@ -323,6 +325,11 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
             return;
         }
     }
+    if (variant == 15) {
+        if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 5>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
     if (variant == 46) {
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 16>), dim3(blocks), dim3(256), 0, s, p);
@@ -333,10 +340,14 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 8>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
-    if (variant == 57 || variant == 58) {
+    if (variant == 58) {
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
-        else if (variant == 57) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 2>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if (variant == 45) {
+        if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 4>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
     if (variant == 48) {  // persistent, next step's loads ahead (the resident workgroups)
@@ -351,8 +362,8 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #endif
-    const bool seg = variant % 64 == 47 || variant == 45;
-    if (mode == MODE_VERIFY) {  // (45: 47's verify; its cached first KiB measured slower there)
+    const bool seg = variant % 64 == 47 || variant == 57;
+    if (mode == MODE_VERIFY) {  // (57: 47's verify)
         hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
@@ -363,7 +374,7 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #endif
-    if (variant == 45) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 4>), dim3(blocks), dim3(256), 0, s, p);
+    if (variant == 57) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
     else if (seg) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true>), dim3(blocks), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
 }

@@ -738,9 +738,11 @@ WIDE_KERNELS = {
     # variant: (kernel name, the largest record length it serves)
     42: ("csum_tile_kernel", 1520),
     44: ("xwalk_kernel", 16257),
+    15: ("xwalk_kernel", 16257),
     45: ("xwalk_kernel", 16257),
     46: ("xwalk_kernel", 16257),
     47: ("xwalk_kernel", 16257),
+    57: ("xwalk_kernel", 16257),
     48: ("xwalk_kernel", 16257),
     59: ("xwalk_kernel", 16257),
 }

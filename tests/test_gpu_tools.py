@@ -70,8 +70,8 @@ def test_last_launch_families(eng):
     eng.emit(buf, b)
     ll = eng.last_launch()
     # packed fixed-stride emit of 1400-1580-B records (not multiples of 64 B): the transposed walk
-    # with each record's first KiB loaded cached
-    assert (ll["kernel"], ll["variant"], ll["G"]) == ("xwalk_kernel", 45, 8), ll
+    # with its field segments stored non-temporal
+    assert (ll["kernel"], ll["variant"], ll["G"]) == ("xwalk_kernel", 57, 8), ll
     eng.verify(buf, b)
     ll = eng.last_launch()
     # packed fixed-stride verify of 1473 .. 8065-B records: the transposed walk, 8 records per wavefront
@@ -79,7 +79,7 @@ def test_last_launch_families(eng):
     X, W = "xwalk_kernel", "csum_kernel"
     for LL, stride, op, want in ((1320, 1320, "verify", (W, 5, 8)), (1500, 1501, "verify", (W, 5, 8)),
                                  (2500, 2500, "emit", (X, 47, 16)), (2500, 2500, "verify", (X, 47, 16)),
-                                 (1500, 1500, "emit", (X, 45, 8)), (1600, 1600, "emit", (W, 39, 8)),
+                                 (1500, 1500, "emit", (X, 57, 8)), (1600, 1600, "emit", (W, 39, 8)),
                                  (1320, 1320, "emit", (W, 39, 8)), (1500, 1564, "emit", (W, 39, 8)), (9000, 9000, "verify", (W, 5, None)),
                                  (8000, 8000, "emit", (X, 47, 32)), (1536, 1536, "verify", (W, 5, 8)), (12000, 12000, "emit", (W, 39, None)),
                                  (12000, 12000, "verify", (W, 5, None)), (2500, 2564, "emit", (X, 47, 16)),
