@@ -706,7 +706,7 @@ def main(argv=None):
     # Emit's floor (rank 0): the read-only stream probe over the TX buffer, and the same stream plus
     # emit's scattered field stores (smol_csum_tool_field_probe: 2-B stores at the records' field
     # offsets, one store event per field per record): the floor of an emit that stores its fields as
-    # 2-B writes.  Fixed-stride emit (variants 39 / 45 / 47) writes most field segments whole and
+    # 2-B writes.  Fixed-stride emit (variants 39 / 47 / 57) writes most field segments whole and
     # runs under it.
     probe = floor = None
     if rank == 0 and wl.copy is None:
@@ -751,7 +751,7 @@ def main(argv=None):
         floor = {"kernel": "field_probe_kernel", "ms": round(fp_ms, 4), "read_only_ms": round(ro_ms, 4),
                  "what": "the 2-B-store reference: the TX buffer streamed once (best read pattern) + " + where
                          + " (emit's store events as 2-B writes, no parse / gates); fixed-stride emit writes "
-                         "whole 64-B field segments (variants 39 / 45 / 47) and runs under it; the bytes the probe "
+                         "whole 64-B field segments (variants 39 / 47 / 57) and runs under it; the bytes the probe "
                          "overwrote are restored"}
 
     unfused = None

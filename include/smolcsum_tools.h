@@ -40,11 +40,11 @@ int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
 /* Kernel variant (-1 = automatic; since round 5: 63 for verify and emit over descriptor batches,
  * the descriptor walk with cached header windows (csum_dwalk.hip; 60 = its non-temporal-window
- * verify); for fixed-stride batches 45 (emit of packed 1400-1580-B records not multiples of 64 B:
- * the transposed walk with each record's first KiB loaded cached), 47 (the transposed walk with
+ * verify); for fixed-stride batches 57 (emit of packed 1400-1580-B records not multiples of 64 B:
+ * the transposed walk with its field segments stored non-temporal), 47 (the transposed walk with
  * whole field segments: verify of packed 1473-1665-B records not multiples of 128 B, verify / emit
  * of 1666-8065-B records), 39 (other fixed-stride emit: variant 5 with whole field segments), 44
- * (47 / 45 under SMOL_BATCH_FIELD_STORES), 5 otherwise; 13 for NHC / data over descriptors; 21 for
+ * (47 / 57 under SMOL_BATCH_FIELD_STORES), 5 otherwise; 13 for NHC / data over descriptors; 21 for
  * copy-emit.  The product library runs these and 7 / 17; libsmolcsum_exp.so every variant below
  * (csum_api.cpp variant_built).  Round 1-4 meanings: 7 was emit over descriptor batches, 13 verify
  * over them, 29 fixed-stride emit.)  The
