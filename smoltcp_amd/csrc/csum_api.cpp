@@ -169,7 +169,8 @@ int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
     if (variant == 47 || variant == 57 || variant == 45) return 44;
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
-    if (variant == 62) return 63;  // (63 stores 2-B fields only)
+    if (variant == 62 || variant == 18) return 63;  // (63 stores 2-B fields only)
+    if (variant == 20) return 60;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
@@ -187,7 +188,7 @@ bool variant_built(int v) {
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 45 || v == 46 || v == 15 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
+           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 45 || v == 46 || v == 15 || v == 18 || v == 20 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
 #else
     return false;
 #endif
@@ -283,7 +284,10 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     // non-temporal-window verify; 56, 60's emit and 61 / 62 (emit with whole field segments) in the
     // experiments build only
 #ifdef SMOL_EXP
-    const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63;
+    const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63 ||
+                        variant == 18 || variant == 20;
+    if (variant == 18 && mode == MODE_VERIFY) variant = 63;  // emit forms of 63 / 60
+    if (variant == 20 && mode == MODE_VERIFY) variant = 60;
     if (variant % 64 == 61 && mode == MODE_VERIFY) variant = 60;  // an emit form of 60
     if (variant == 62 && mode == MODE_VERIFY) variant = 63;      // an emit form of 63
     // (forced, the experiments build also runs it over fixed-stride batches)

@@ -48,7 +48,8 @@ constexpr int U = 4;        // load instructions in flight per wavefront
 // window, the fields patched in, as the walk kernel's variant 39 does for fixed strides (§5 of
 // a whole segment is a plain write at the memory side, a 2-B store a read-modify-write).
 // SEGF bit 0: whole segments (variant 61); bit 1: the header windows loaded with the default cache
-// policy instead of non-temporal (62 = both, 63 = bit 1 alone, experiments).
+// policy instead of non-temporal (62 = both, 63 = bit 1 alone); bit 2: the 2-B fields stored
+// non-temporal (experiments: 18 = 63 + bit 2, 20 = 60's emit + bit 2).
 template <int MODE, bool NOSTORE, bool GROUPS = false, int SEGF = 0>
 __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     using namespace dwalk;
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
         if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
         if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
     } else {
-        if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane);
+        if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE, (SEGF & 4) != 0>(p, g, a1, rd, winb, hd, a0, r, lane);
     }
 }
 
@@ -291,6 +292,8 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
             hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false, true>), dim3(b), dim3(256), 0, s, q);
 #ifdef SMOL_EXP
         else if (variant == 60) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 18) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 6>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 20) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 4>), dim3(b), dim3(256), 0, s, q);
         else if (variant == 61) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 1>), dim3(b), dim3(256), 0, s, q);
         else if (variant == 62) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 3>), dim3(b), dim3(256), 0, s, q);
         else if (variant == 64 + 61) hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, true, true, 1>), dim3(b), dim3(256), 0, s, q);

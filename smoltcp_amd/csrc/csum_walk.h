@@ -347,11 +347,20 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Store a big-endian u16 at any byte alignment.  NOSTORE (experiment variants only): the value
-// computed and kept live, nothing stored.
-template <bool NOSTORE = false>
+// computed and kept live, nothing stored.  NT (experiment variants only): non-temporal stores.
+template <bool NOSTORE = false, bool NT = false>
 __device__ __forceinline__ void store_be16(gu8 q, uint32_t v) {
     if constexpr (NOSTORE) {
         asm volatile("" ::"v"(v), "v"(q));
+        return;
+    }
+    if constexpr (NT) {
+        if (((uint64_t)q & 1u) == 0) {
+            __builtin_nontemporal_store((uint16_t)bswap16(v), (gu16)q);
+        } else {
+            __builtin_nontemporal_store((uint8_t)(v >> 8), q);
+            __builtin_nontemporal_store((uint8_t)v, q + 1);
+        }
         return;
     }
     if (((uint64_t)q & 1u) == 0) {
@@ -429,7 +438,8 @@ __device__ __forceinline__ void emit_fields(const Geom& g, uint32_t f[3]) {
 // SEGP (fixed-stride emit, SEGW): the 64-B segments wsA / wsB (~0: none) go out whole from the
 // window afterwards; a field is patched into the window, and stored to global memory unless both
 // of its bytes lie in those segments.
-template <int G, int MODE, bool NHC, class RD, int WINB = 0, bool SEGP = false, bool NOSTORE = false>
+template <int G, int MODE, bool NHC, class RD, int WINB = 0, bool SEGP = false, bool NOSTORE = false,
+          bool NTST = false>
 __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, uint32_t acc, const RD& rd,
                                              const uint8_t* winb, uint32_t head, uint64_t a0, uint64_t r,
                                              int lane, uint8_t* winw = nullptr, uint64_t wsA = ~0ull,
@@ -594,9 +604,9 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
             if (fl4 != MF_NONE) put(fl4, vl4);
             if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
         } else if (EMITS) {
-            if (fip != MF_NONE) store_be16<NOSTORE>(wrec + fip, vip);
-            if (fin != MF_NONE) store_be16<NOSTORE>(wrec + fin, vin);
-            if (fl4 != MF_NONE) store_be16<NOSTORE>(wrec + fl4, vl4);
+            if (fip != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fip, vip);
+            if (fin != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fin, vin);
+            if (fl4 != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fl4, vl4);
             if (NHC && nb0 != NO_FIELD) wrec[0] = (uint8_t)nb0;
             if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
         } else {
