@@ -188,7 +188,7 @@ bool variant_built(int v) {
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 45 || v == 46 || v == 15 || v == 18 || v == 20 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
+           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 45 || v == 46 || v == 15 || v == 18 || v == 20 || v == 22 || v == 30 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
 #else
     return false;
 #endif
@@ -332,7 +332,7 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
             if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
             return SMOL_OK;
         }
-        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17) ? cv : 21;
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17 || cv == 22 || cv == 30) ? cv : 21;
         const int cshape = ctx->shape >= 0 ? ctx->shape : ((var == 17 || var == 21) ? (int)CFG_G16U4 : shape);
         hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
         if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");

@@ -71,7 +71,9 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 // LBS (variant 21): the first body round's loads are issued right after the parse, before round 1's
 // chunk stores, so that waiting for them does not also wait for those stores (gfx950 counts stores
 // in vmcnt, in issue order with the loads).
-template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0, bool LBS = false>
+// NTB (experiments build): bit 0 the body chunks stored non-temporal (variant 30), bit 1 also the
+// body's source chunks loaded non-temporal (variant 22).
+template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0, bool LBS = false, int NTB = 0>
 __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
     constexpr int GPB = 256 / G;
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
         auto body_load1 = [&](uint32_t i, u32x4& lo, uint32_t& hi) {
             const bool in = i < nb;
             const uint64_t A = skA + 16ull * (kb0 + i);
-            lo = ld16<false>((gcv4)(in ? A : dummy));
+            lo = ld16<(NTB & 2) != 0>((gcv4)(in ? A : dummy));
             hi = need_hi ? *(const GMEM uint32_t*)(in && b ? A + 16 : dummy) : 0u;
         };
         auto body_load = [&](uint32_t i0, u32x4* lo, uint32_t* hi) {
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
                 const uint32_t i = i0 + (uint32_t)(u * G + lane);
                 const bool in = i < nb;
                 const uint64_t A = skA + 16ull * (kb0 + i);
-                lo[u] = ld16<false>((gcv4)(in ? A : dummy));
+                lo[u] = ld16<(NTB & 2) != 0>((gcv4)(in ? A : dummy));
                 // (b == 0: that dword may lie past the source range, so it is not read)
                 hi[u] = need_hi ? *(const GMEM uint32_t*)(in && b ? A + 16 : dummy) : 0u;
             }
@@ -280,8 +282,10 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             const int pos = (int)(16u * k) - (int)head;
             acc = sum_chunk(m, pos, s1, acc);
             const gu8 dst = (gu8)base + 16u * k;
-            if (!far) *(GMEM u32x4*)dst = m;
-            else store_part(dst, m, 0, 16, f0b - pos, f1b - pos, f2b - pos);
+            if (!far) {
+                if constexpr ((NTB & 1) != 0) __builtin_nontemporal_store(m, (GMEM u32x4*)dst);
+                else *(GMEM u32x4*)dst = m;
+            } else store_part(dst, m, 0, 16, f0b - pos, f1b - pos, f2b - pos);
         };
         if constexpr (UB > 0) {
 #pragma unroll
@@ -311,13 +315,13 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     }
 }
 
-template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0, bool LBS = false>
+template <bool IMPLICIT, int G, int U, int UW = 0, int UB = 0, bool LBS = false, int NTB = 0>
 hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s) {
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    note_launch(KERN_COPY, LBS ? 21 : 17, G, U);
-    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB, LBS>), dim3(blocks), dim3(256), 0, s, p);
+    note_launch(KERN_COPY, NTB == 1 ? 30 : NTB == 3 ? 22 : LBS ? 21 : 17, G, U);
+    hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB, LBS, NTB>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -361,5 +365,18 @@ hipError_t launch_copy_v21(int shape, const KParams& p, uint32_t max_blocks, hip
     return im ? launch_copy2_one<true, 16, 4, 1, 2, true>(p, max_blocks, s)
               : launch_copy2_one<false, 16, 4, 1, 2, true>(p, max_blocks, s);
 }
+
+#ifdef SMOL_EXP
+// variants 30 / 22 (experiments build): variant 21 at 16 x 4 with non-temporal body stores / and
+// non-temporal body source loads.
+hipError_t launch_copy_nt(int var, const KParams& p, uint32_t max_blocks, hipStream_t s) {
+    const bool im = p.desc == nullptr;
+    if (var == 30)
+        return im ? launch_copy2_one<true, 16, 4, 1, 2, true, 1>(p, max_blocks, s)
+                  : launch_copy2_one<false, 16, 4, 1, 2, true, 1>(p, max_blocks, s);
+    return im ? launch_copy2_one<true, 16, 4, 1, 2, true, 3>(p, max_blocks, s)
+              : launch_copy2_one<false, 16, 4, 1, 2, true, 3>(p, max_blocks, s);
+}
+#endif
 
 }  // namespace smolcsum

@@ -1418,6 +1418,10 @@ hipError_t launch_copy_var(int shape, const KParams& p, uint32_t max_blocks, hip
 hipError_t launch_copy_v17(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s);
 // variant 21: variant 17 with the first body round's loads ahead of round 1's stores (csum_copy.hip)
 hipError_t launch_copy_v21(int shape, const KParams& p, uint32_t max_blocks, hipStream_t s);
+#ifdef SMOL_EXP
+// variants 30 / 22: 21 with non-temporal body stores / and source loads (csum_copy.hip)
+hipError_t launch_copy_nt(int var, const KParams& p, uint32_t max_blocks, hipStream_t s);
+#endif
 
 // 17 / 21 (copy_kernel) are the product's; the walk kernel's MODE_COPY variants (1, 8, 11, 16: the
 // round-1 / 2 designs) are in the experiments build only.
@@ -1427,6 +1431,8 @@ hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks
         case 17: return launch_copy_v17(shape, p, max_blocks, s);
         case 21: return launch_copy_v21(shape, p, max_blocks, s);
 #ifdef SMOL_EXP
+        case 30:
+        case 22: return launch_copy_nt(var, p, max_blocks, s);
         case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
         case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);
         case 8: return launch_copy_var<IMPLICIT, 8>(shape, p, max_blocks, s);

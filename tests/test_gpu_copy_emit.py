@@ -118,7 +118,8 @@ def _run(eng, recs, copies_spec, caps=(0, 0, 0, 0, 0), shape=-1, fixed_stride=No
         eng.set_variant(-1)
         eng.set_max_blocks(0)
     if n:  # the forced variant ran its own kernel (default: copy_kernel variant 21)
-        want = ("csum_kernel", variant) if variant in (1, 8, 11, 16) else ("copy_kernel", 17 if variant == 17 else 21)
+        want = ("csum_kernel", variant) if variant in (1, 8, 11, 16) else \
+            ("copy_kernel", variant if variant in (17, 22, 30) else 21)
         if variant in (49, 50, 55) and fixed_stride and 1024 <= (fixed_len or fixed_stride) <= 1921:
             want = ("copy_kernel", variant)  # the transposed layout (csum_xcopy.hip)
         assert (launched["kernel"], launched["variant"]) == want, (variant, launched)
@@ -226,7 +227,7 @@ def test_xcopy_fast_layout(eng, stride, length, variant):
         _run(eng, recs, mixed, fixed_stride=stride, fixed_len=length, variant=variant, base=base, seed=n + 1)
 
 
-COPY_VARIANTS = [-1, 1, 8, 11, 16, 17, 21]
+COPY_VARIANTS = [-1, 1, 8, 11, 16, 17, 21, 22, 30]
 
 
 @pytest.mark.parametrize("variant", COPY_VARIANTS)
