@@ -38,9 +38,9 @@ int smol_csum_tool_corrupt(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum
  * 0: 8 x 6, 1: 16 x 3, 2: 16 x 6, 3: 32 x 3, 4: 32 x 4, 5: 64 x 2, 6: 64 x 4, 7: 8 x 7, 8: 16 x 4. */
 int smol_csum_tool_set_shape(smol_csum_ctx_t* ctx, int shape);
 
-/* Kernel variant (-1 = automatic; since round 5: 63 for verify and emit over descriptor batches,
- * the descriptor walk with cached header windows (csum_dwalk.hip; 60 = its non-temporal-window
- * verify); for fixed-stride batches 57 (emit of packed 1400-1580-B records not multiples of 64 B:
+/* Kernel variant (-1 = automatic; since round 5: 63 for verify over descriptor batches, the
+ * descriptor walk with cached header windows (csum_dwalk.hip; 60 = its non-temporal-window verify),
+ * 41 for emit over them (63 with the window's chunks summed from LDS); for fixed-stride batches 57 (emit of packed 1400-1580-B records not multiples of 64 B:
  * the transposed walk with its field segments stored non-temporal), 47 (the transposed walk with
  * whole field segments: verify of packed 1473-1665-B records not multiples of 128 B, verify / emit
  * of 1666-8065-B records), 39 (other fixed-stride emit: variant 5 with whole field segments), 44

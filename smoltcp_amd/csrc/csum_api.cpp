@@ -111,8 +111,13 @@ int walk_variant(int mode, bool has_desc) {
 // (profiles/r05_experiments/dwalk_cached_windows.txt); its emit beats the tile kernel on every
 // descriptor layout measured, 64-1500-B records 0.223 -> 0.184 ms.  The tile kernel stays the
 // descriptor-emit fallback (NHC emit runs the walk kernel).
+// Its emit form 41 sums the 16 window chunks from LDS and streams from chunk 16 (the window lines not
+// read a second time): C3 emit 0.894 -> 0.881 ms, shuffled descriptors 0.922 -> 0.912, 64-1500-B
+// records 0.186 -> 0.183; its verify measured 0.4 % slower, so verify stays on 63
+// (profiles/r05_experiments/dwalk_cached_windows.txt).
 int auto_variant(int mode, bool has_desc) {
-    if ((mode == MODE_VERIFY || mode == MODE_EMIT) && has_desc) return 63;
+    if (mode == MODE_EMIT && has_desc) return 41;
+    if (mode == MODE_VERIFY && has_desc) return 63;
     return walk_variant(mode, has_desc);
 }
 
@@ -171,6 +176,7 @@ int field_store_variant(int variant, bool has_desc) {
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62 || variant == 18) return 63;  // (63 stores 2-B fields only)
     if (variant == 20) return 60;
+    if (variant == 41) return 41;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
@@ -181,14 +187,14 @@ int field_store_variant(int variant, bool has_desc) {
 // field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
 bool variant_built(int v) {
     switch (v) {
-        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 44: case 47: case 57: case 60: case 63: return true;
+        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 41: case 44: case 47: case 57: case 60: case 63: return true;
         default: break;
     }
 #ifdef SMOL_EXP
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
-           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 45 || v == 46 || v == 15 || v == 18 || v == 20 || v == 22 || v == 30 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
+           (v >= 31 && v <= 38) || v == 40 || v == 12 || v == 14 || v == 42 || v == 43 || v == 45 || v == 46 || v == 15 || v == 18 || v == 20 || v == 22 || v == 30 || v == 41 || v == 48 || (v >= 49 && v <= 59) || v == 61 || v == 62;
 #else
     return false;
 #endif
@@ -280,12 +286,13 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
                         variant == 58 || variant == 59;
     const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
     if (xw_var && !xwalk) variant = fallback;
-    // descriptor-batch walks: 63 = verify / emit default (cached header windows), 60 = its
+    if (variant == 41 && mode == MODE_VERIFY) variant = 63;  // 41: the emit form of 63
+    // descriptor-batch walks: 63 = verify default (cached header windows), 41 = emit default, 60 = its
     // non-temporal-window verify; 56, 60's emit and 61 / 62 (emit with whole field segments) in the
     // experiments build only
 #ifdef SMOL_EXP
     const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63 ||
-                        variant == 18 || variant == 20;
+                        variant == 18 || variant == 20 || variant == 41;
     if (variant == 18 && mode == MODE_VERIFY) variant = 63;  // emit forms of 63 / 60
     if (variant == 20 && mode == MODE_VERIFY) variant = 60;
     if (variant % 64 == 61 && mode == MODE_VERIFY) variant = 60;  // an emit form of 60
@@ -293,8 +300,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     // (forced, the experiments build also runs it over fixed-stride batches)
     const bool dwalk = dw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs;
 #else
-    const bool dw_var = variant == 60 || variant == 63;
-    const bool dwalk = dw_var && (mode == MODE_VERIFY || (mode == MODE_EMIT && variant == 63)) && has_desc && !d_addrs;
+    const bool dw_var = variant == 60 || variant == 63 || variant == 41;
+    const bool dwalk = dw_var && (mode == MODE_VERIFY || (mode == MODE_EMIT && variant != 60)) && has_desc && !d_addrs;
 #endif
     if (dw_var && !dwalk) variant = fallback;
     const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
@@ -651,7 +658,7 @@ const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int h
         return (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? "csum_kernel" : "copy_kernel";
     }
     const int v = ctx->variant >= 0 ? ctx->variant : auto_variant(op, has_desc != 0);
-    if (has_desc && ((v == 60 && op == MODE_VERIFY) || (v == 63 && (op == MODE_VERIFY || op == MODE_EMIT))))
+    if (has_desc && ((v == 60 && op == MODE_VERIFY) || ((v == 63 || v == 41) && (op == MODE_VERIFY || op == MODE_EMIT))))
         return "dwalk_kernel";
     const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY);
     return tile ? "csum_tile_kernel" : "csum_kernel";

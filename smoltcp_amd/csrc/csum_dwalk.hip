@@ -49,7 +49,9 @@ constexpr int U = 4;        // load instructions in flight per wavefront
 // a whole segment is a plain write at the memory side, a 2-B store a read-modify-write).
 // SEGF bit 0: whole segments (variant 61); bit 1: the header windows loaded with the default cache
 // policy instead of non-temporal (62 = both, 63 = bit 1 alone); bit 2: the 2-B fields stored
-// non-temporal (experiments: 18 = 63 + bit 2, 20 = 60's emit + bit 2).
+// non-temporal (experiments: 18 = 63 + bit 2, 20 = 60's emit + bit 2); bit 3: the window's 16
+// chunks summed from LDS, the stream starting at chunk 16 (41 = 63 + bit 3: the product's
+// descriptor-batch emit since late round 5).
 template <int MODE, bool NOSTORE, bool GROUPS = false, int SEGF = 0>
 __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     using namespace dwalk;
@@ -230,7 +232,21 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
         const int s1 = mine && l4 ? (int)g.span_end : 0;
         const uint64_t base = a0 & ~127ull;
         const uint32_t nch = (uint32_t)((int)hd + s1 + 15) >> 4;  // chunks up to the span's end
-        for (uint32_t c0 = 0; c0 < nch; c0 += (uint32_t)(G * U)) {
+        uint32_t cstart = 0;
+        if constexpr ((SEGF & 8) != 0) {  // the window's chunks from LDS, the stream from chunk 16
+#pragma unroll
+            for (int h = 0; h < WIN_CH / G; ++h) {
+                const uint32_t c = (uint32_t)(G * h + lane);
+                const int pos = 16 * (int)c - (int)hd;
+                if (c < nch) {
+                    const u32x4 x = win[gib][c];
+                    if (pos >= 0 && pos + 16 <= s1) a1 = add_words(x.x, add_words(x.y, add_words(x.z, add_words(x.w, a1))));
+                    else a1 = sum_masked_words(x, -pos, s1 - pos, a1);
+                }
+            }
+            cstart = WIN_CH;
+        }
+        for (uint32_t c0 = cstart; c0 < nch; c0 += (uint32_t)(G * U)) {
             u32x4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -270,8 +286,9 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
 
 hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) {
 #ifndef SMOL_EXP
-    // the product's forms: 63 (verify / emit), 60 (verify)
-    if (!(variant == 63 && (mode == MODE_VERIFY || mode == MODE_EMIT)) && !(variant == 60 && mode == MODE_VERIFY))
+    // the product's forms: 63 (verify / emit), 41 (emit), 60 (verify)
+    if (!(variant == 63 && (mode == MODE_VERIFY || mode == MODE_EMIT)) && !(variant == 60 && mode == MODE_VERIFY) &&
+        !(variant == 41 && mode == MODE_EMIT))
         return hipErrorInvalidValue;
 #endif
     const uint64_t per = (uint64_t)dwalk::GPB;
@@ -288,6 +305,8 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
             hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false, true, 2>), dim3(b), dim3(256), 0, s, q);
         else if (variant == 63)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 2>), dim3(b), dim3(256), 0, s, q);
+        else if (variant == 41)
+            hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10>), dim3(b), dim3(256), 0, s, q);
         else if (variant == 60 && mode == MODE_VERIFY)
             hipLaunchKernelGGL((dwalk_kernel<MODE_VERIFY, false, true>), dim3(b), dim3(256), 0, s, q);
 #ifdef SMOL_EXP

@@ -70,9 +70,9 @@ def _run_records(eng, records, kinds, caps=CAPS_DEFAULT, gap_seed=None, shape=-1
         diff = np.nonzero(got != ref)[0]
         assert diff.size == 0, f"emit bytes differ at {diff[:8]}"
         assert np.array_equal(est.cpu().numpy(), ref_est), "emit status differs"
-        if variant in (56, 60, 63) and len(records):  # verify ran the descriptor walk it names
-            assert (launched_v["kernel"], launched_v["variant"]) == ("dwalk_kernel", variant), launched_v
-        if variant in (61, 62, 63, 18, 20) and len(records):  # so did emit
+        if variant in (56, 60, 63, 41) and len(records):  # verify ran the descriptor walk it names
+            assert (launched_v["kernel"], launched_v["variant"]) == ("dwalk_kernel", 63 if variant == 41 else variant), launched_v
+        if variant in (61, 62, 63, 18, 20, 41) and len(records):  # so did emit
             assert (launched_e["kernel"], launched_e["variant"]) == ("dwalk_kernel", variant), launched_e
         return st, got, offs, lens
     finally:
@@ -282,7 +282,7 @@ def _mixed_records(rng, n=240):
     return recs
 
 
-@pytest.mark.parametrize("variant", [56, 60, 61, 62, 63, 18, 20])
+@pytest.mark.parametrize("variant", [56, 60, 61, 62, 63, 18, 20, 41])
 def test_dwalk_descriptor_batches(eng, variant):
     """The descriptor walks (63: the product's descriptor verify / emit, cached header windows; 60:
     non-temporal windows; experiments build: 56, and 61 / 62 = 60's / 63's emit with whole field

@@ -96,7 +96,7 @@ def test_last_launch_families(eng):
     # 8 lanes x 4 chunks, both operations; the tile kernel when forced (variant 7)
     eng.emit(buf, bd)
     ll = eng.last_launch()
-    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 63, 8, 4), ll
+    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 41, 8, 4), ll
     eng.verify(buf, bd)
     ll = eng.last_launch()
     assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 63, 8, 4), ll
