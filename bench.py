@@ -505,6 +505,45 @@ def cpu_baseline(E, wl, seconds: float):
     return out, parity
 
 
+def parity_spread(E, wl, records: int = 65536, windows: int = 64) -> dict:
+    """The oracle check without timing, over `records` records sampled across the WHOLE batch (`windows`
+    runs of consecutive records, evenly spaced from the first record to the last): the oracle's emit of
+    each run (emit is idempotent) must reproduce the device's emitted TX bytes, and its verify of the
+    RX bytes the device's status bytes, bit for bit.  Runs on every config, with or without the CPU
+    baseline (whose sample is the batch's first 1.6 GB)."""
+    import oracle
+
+    n = wl.n
+    per = max(1, min(n, records) // windows)
+    starts = sorted({int(x) for x in np.linspace(0, max(0, n - per), windows)})
+    desc_all = wl.batch.desc.cpu().numpy().view(E.DESC_DTYPE) if wl.batch.desc is not None else None
+    stride, L = (wl.batch.stride, wl.batch.length) if desc_all is None else (0, 0)
+    st_all = wl.status.cpu().numpy()
+    checked, emit_ok, verify_ok = 0, True, True
+    for lo in starts:
+        hi = min(n, lo + per)
+        if desc_all is None:
+            a, b, d = lo * stride, (hi - 1) * stride + L, None
+        else:
+            d = desc_all[lo:hi].copy()
+            a = int(d["offset"].min())
+            b = int((d["offset"] + d["len"].astype(np.uint64)).max())
+            d["offset"] -= np.uint64(a)
+        tx = wl.tx[a:b].cpu().numpy()
+        rx = wl.rx[a:b].cpu().numpy()
+        ref = tx.copy()
+        oracle.batch_emit(ref, d, hi - lo, stride, L, wl.kind, (0, 0, 0, 0, 0))
+        emit_ok &= bool(np.array_equal(ref, tx))
+        st = oracle.batch_verify(rx.copy(), d, hi - lo, stride, L, wl.kind, (0, 0, 0, 0, 0))
+        verify_ok &= bool(np.array_equal(st, st_all[lo:hi]))
+        checked += hi - lo
+    return {"records": checked, "windows": len(starts), "emit_bitexact": emit_ok, "verify_bitexact": verify_ok,
+            "checker": "oracle/csum_oracle.c",
+            "sample": f"{len(starts)} runs of {per} consecutive records evenly spaced over all {n} records "
+                      f"(first run at record 0, last ending at record {n - 1}): emit of TX batch 0, verify of RX "
+                      f"batch 0 (the last verify's status)"}
+
+
 def _launch_name(ll):
     """'xwalk_kernel v47 G8 U2' from an engine.last_launch() record."""
     return "?" if not ll else f"{ll['kernel']} v{ll['variant']} G{ll['G']} U{ll['U']}"
@@ -704,10 +743,10 @@ def main(argv=None):
     per = gather_floats([rank, local, mine, emit_ms, verify_ms, rejected], device=dev)
 
     # Emit's floor (rank 0): the read-only stream probe over the TX buffer, and the same stream plus
-    # emit's scattered field stores (smol_csum_tool_field_probe: 2-B stores at the records' field
-    # offsets, one store event per field per record): the floor of an emit that stores its fields as
-    # 2-B writes.  Fixed-stride emit (variants 39 / 47 / 57) writes most field segments whole and
-    # runs under it.
+    # emit's writes in emit's own shape (smol_csum_tool_segment_probe: every 64-B segment holding a
+    # checksum field written back whole, with its own bytes, by the lanes that just read it; plain and
+    # non-temporal stores, the faster is the floor).  floor_2b: the same stream plus a 2-B store at
+    # every field instead (smol_csum_tool_field_probe / _list, the floor of a 2-B-store emit).
     probe = floor = None
     if rank == 0 and wl.copy is None:
         sink = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -724,10 +763,13 @@ def main(argv=None):
             return a.elapsed_time(b) / reps
 
         ro_ms = timed(lambda: eng.stream_read(wl.tx, sink, stream=stream))
-        # the probe stores into wl.tx: the bytes it overwrites are saved first and put back after it
-        # (emit is not a restore: on C3 / C4 the probe's offsets are not all checksum fields)
         addrs = field_addrs(wl)
         nb = wl.tx.numel() // 16 * 16
+        bitmap, nseg = E.segment_bitmap(addrs, nb)
+        seg_ms = {nt: timed(lambda: eng.segment_probe(wl.tx, bitmap, nt=nt, stream=stream)) for nt in (False, True)}
+        del bitmap
+        # the 2-B probe stores into wl.tx: the bytes it overwrites are saved first and put back after it
+        # (emit is not a restore: on C3 / C4 the probe's offsets are not all checksum fields)
         pieces = torch.arange(0, (nb + 8191) // 8192 + 1, device=dev, dtype=torch.int64) * 8192
         first = torch.searchsorted(addrs, pieces).to(torch.int32)
         del pieces
@@ -745,14 +787,20 @@ def main(argv=None):
         del saved
         del addrs, first
         torch.cuda.synchronize()
-        nbytes = wl.tx.numel() // 16 * 16
-        probe = {"kernel": "stream_read_kernel", "bytes": nbytes, "ms": round(ro_ms, 4),
-                 "GB/s": round(nbytes / ro_ms / 1e6, 1)}
-        floor = {"kernel": "field_probe_kernel", "ms": round(fp_ms, 4), "read_only_ms": round(ro_ms, 4),
-                 "what": "the 2-B-store reference: the TX buffer streamed once (best read pattern) + " + where
-                         + " (emit's store events as 2-B writes, no parse / gates); fixed-stride emit writes "
-                         "whole 64-B field segments (variants 39 / 47 / 57) and runs under it; the bytes the probe "
-                         "overwrote are restored"}
+        probe = {"kernel": "stream_read_kernel", "bytes": nb, "ms": round(ro_ms, 4),
+                 "GB/s": round(nb / ro_ms / 1e6, 1)}
+        best_nt = seg_ms[True] <= seg_ms[False]
+        floor = {"kernel": "segment_probe_kernel", "ms": round(min(seg_ms.values()), 4),
+                 "stores": "non-temporal" if best_nt else "plain",
+                 "ms_plain_stores": round(seg_ms[False], 4), "ms_nt_stores": round(seg_ms[True], 4),
+                 "segments": nseg, "read_only_ms": round(ro_ms, 4),
+                 "what": f"emit's floor in its store shape: the TX buffer streamed once (the stream-read probe's "
+                         f"pattern) + the {nseg} 64-B segments holding its checksum fields written back whole with "
+                         f"their own bytes by the lanes that just read them (no parse / gates); the faster of plain "
+                         f"and non-temporal stores"}
+        floor_2b = {"kernel": "field_probe_kernel", "ms": round(fp_ms, 4),
+                    "what": "the 2-B-store reference: the same stream + " + where
+                            + " (emit's store events as 2-B writes); the bytes the probe overwrote are restored"}
 
     unfused = None
     if wl.copy is not None and rank == 0:
@@ -777,6 +825,9 @@ def main(argv=None):
     cpu, parity = None, None
     if rank == 0 and world == 1 and wl.copy is None:
         cpu, parity = cpu_baseline(E, wl, args.cpu_seconds)
+    if rank == 0 and wl.copy is None:
+        spread = parity_spread(E, wl)
+        parity = dict(parity or {}, spread=spread) if parity else {"spread": spread}
 
     if rank == 0:
         value = S.aggregate_rate(2 * wl.span_bytes, world, args.steps, elapsed)
@@ -842,6 +893,8 @@ def main(argv=None):
         if floor and dom == "emit":
             out["roofline"]["floor"] = floor
             out["roofline"]["floor_frac"] = round(floor["ms"] / kd["ms"], 4)
+            out["roofline"]["floor_2b"] = floor_2b
+            out["roofline"]["floor_2b_frac"] = round(floor_2b["ms"] / kd["ms"], 4)
         if probe and dom in ("emit", "verify"):
             # the dominant kernel against the read-only stream over the same bytes (1.0 = it runs at
             # the speed of reading its input once at the best pattern)

@@ -109,6 +109,14 @@ int smol_csum_tool_field_probe(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t by
  * offset with the values it holds (the store shape of whole-segment emit; nothing changes). */
 int smol_csum_tool_field_probe_list(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
                                     const uint32_t* d_piece_first, int flags, void* stream);
+/* Emit's floor in emit's store shape: the stream-read probe over `bytes`, and every 64-byte segment
+ * whose bit is set in `d_bitmap` (one bit per 64-byte segment of the buffer: bit s % 32 of word s / 32;
+ * ceil(bytes / 8192) * 4 words, 16-byte aligned) written back whole with the bytes just read, by the
+ * lanes that loaded it, right after the 8-KiB piece holding it has been read (nothing changes).
+ * `flags` bit 0: the segments stored non-temporal.  Segments in the tail past the last whole 8-KiB
+ * piece are read, not written. */
+int smol_csum_tool_segment_probe(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint32_t* d_bitmap, int flags,
+                                 void* stream);
 /* A separate store pass (experiments: what emit's field stores cost outside the read stream):
  * for i < n, the big-endian 2-byte value d_vals[i] at byte offset d_addrs[i] of the buffer, one
  * thread per store.  `flags` bit 0: non-temporal stores; bits 1 / 2 / 3: instead write the whole
@@ -119,13 +127,21 @@ int smol_csum_tool_field_scatter(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t 
 /* The launch shape the library picks for a verify over an implicit batch of `len`-byte records. */
 int smol_csum_tool_auto_shape(uint32_t len, int has_desc);
 
-/* The kernel (the rocprofv3 name prefix: "csum_kernel" or "csum_tile_kernel") that an IP-path
- * operation runs with this context's variant setting: op 0 data, 1 emit, 2 verify, 3 copy-emit. */
+/* The kernel (the rocprofv3 name prefix: "csum_kernel", "csum_tile_kernel", "xwalk_kernel",
+ * "dwalk_kernel", "copy_kernel" or "xcopy_kernel") that an IP-path operation on `batch` runs with this
+ * context's variant setting: op 0 data, 1 emit, 2 verify, 3 copy-emit.  The same choice as the
+ * batched entry points make (one dispatch function, csum_api.cpp pick_kernel). */
+const char* smol_csum_tool_kernel_for(const smol_csum_ctx_t* ctx, int op, const smol_csum_batch_t* batch);
+/* Deprecated (kept for old scripts): smol_csum_tool_kernel_for without the batch, so without its record
+ * length — exact for descriptor batches; for fixed-stride batches it names the kernel of short records,
+ * not the transposed walk that serves 1400-8065-B ones.  Use smol_csum_tool_kernel_for or
+ * smol_csum_tool_last_launch. */
 const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int has_desc);
 
 /* The kernel instantiation of this process's last checksum launch (any context), packed as
  * kernel << 24 | variant << 16 | G << 8 | U; kernel 1 = csum_kernel, 2 = csum_tile_kernel,
- * 3 = copy_kernel, 4 = csum_kernel with the 6LoWPAN NHC gates; 0 before the first launch. */
+ * 3 = copy_kernel, 4 = csum_kernel with the 6LoWPAN NHC gates, 5 = xwalk_kernel, 6 = dwalk_kernel;
+ * 0 before the first launch. */
 uint32_t smol_csum_tool_last_launch(void);
 
 /* 1 when this build of the library runs kernel variant `variant` (smol_csum_tool_set_variant), else

@@ -40,9 +40,13 @@ TOOL_SYMBOLS = [
     "smol_csum_tool_set_max_blocks", "smol_csum_tool_auto_shape", "smol_csum_tool_stream_read",
     "smol_csum_tool_set_xcd_remap", "smol_csum_tool_set_launch_records",
     "smol_csum_tool_field_probe",
-    "smol_csum_tool_field_probe_list", "smol_csum_tool_field_scatter", "smol_csum_tool_variant_built",
-    "smol_csum_tool_kernel_name", "smol_csum_tool_last_launch",
+    "smol_csum_tool_field_probe_list", "smol_csum_tool_segment_probe", "smol_csum_tool_field_scatter",
+    "smol_csum_tool_variant_built",
+    "smol_csum_tool_kernel_name", "smol_csum_tool_kernel_for", "smol_csum_tool_last_launch",
 ]
+# Tool symbols added in later rounds: bound only when the loaded build has them (SMOLCSUM_LIB may name
+# an older build for an A/B run), and a call to a missing one raises AttributeError naming it.
+OPTIONAL_TOOL_SYMBOLS = ("smol_csum_tool_variant_built", "smol_csum_tool_kernel_for", "smol_csum_tool_segment_probe")
 
 
 class SmolError(RuntimeError):
@@ -159,8 +163,15 @@ def lib(path: str | None = None) -> ctypes.CDLL:
     L.smol_csum_tool_kernel_name.restype = ctypes.c_char_p
     L.smol_csum_tool_last_launch.argtypes = []
     L.smol_csum_tool_last_launch.restype = u32
-    L.smol_csum_tool_variant_built.argtypes = [i32]
-    L.smol_csum_tool_variant_built.restype = i32
+    if hasattr(L, "smol_csum_tool_variant_built"):
+        L.smol_csum_tool_variant_built.argtypes = [i32]
+        L.smol_csum_tool_variant_built.restype = i32
+    if hasattr(L, "smol_csum_tool_segment_probe"):
+        L.smol_csum_tool_segment_probe.argtypes = [vp, vp, u64, vp, ctypes.c_int, vp]
+        L.smol_csum_tool_segment_probe.restype = i32
+    if hasattr(L, "smol_csum_tool_kernel_for"):
+        L.smol_csum_tool_kernel_for.argtypes = [vp, i32, vp]
+        L.smol_csum_tool_kernel_for.restype = ctypes.c_char_p
     _LIBS[path] = L
     return L
 

@@ -27,6 +27,8 @@ struct smol_csum_ctx {
     int xcd_remap;        // walk kernel: each XCD's blocks take a contiguous range of records
                           // (-1: automatic, xcd_remap_auto; 0 / 1: forced, tooling)
     uint64_t launch_records;  // records per kernel launch (0: the whole batch in one launch)
+    uint64_t* stage;          // staged emit's field entries (variants 80 / 81), grown on first use
+    uint64_t stage_cap;       // entries `stage` holds
 };
 
 namespace smolcsum {
@@ -172,7 +174,7 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
-    if (variant == 47 || variant == 57 || variant == 45) return 44;
+    if (variant == 47 || variant == 57 || variant == 45 || (variant >= 80 && variant <= 86)) return 44;
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62 || variant == 18) return 63;  // (63 stores 2-B fields only)
     if (variant == 20) return 60;
@@ -182,15 +184,17 @@ int field_store_variant(int variant, bool has_desc) {
 }
 
 // The kernel variants this build runs (smol_csum_tool_variant_built).  The product library: the
-// defaults (walk 5 / 39, transposed walk 47, descriptor walk 60, tile 7, copy 21) and one fallback
-// each (copy 17; walk 13 for NHC / data over descriptors and for forced variants; 44 = 47 with 2-B
-// field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
+// defaults (walk 5 / 39, transposed walk 47 / 57, descriptor walk 63 (verify) / 41 (emit), copy 21)
+// and one fallback each (descriptor walk 60, tile 7, copy 17; walk 13 for NHC / data over
+// descriptors and for forced variants; 44 = 47 / 57 with 2-B field stores, SMOL_BATCH_FIELD_STORES).  The experiments build (SMOL_EXP, libsmolcsum_exp.so): every measured variant.
 bool variant_built(int v) {
     switch (v) {
-        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 41: case 44: case 47: case 57: case 60: case 63: return true;
+        case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 41: case 44: case 47: case 57: case 60: case 63:
+            return true;
         default: break;
     }
 #ifdef SMOL_EXP
+    if (v >= 80 && v <= 86) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -234,6 +238,99 @@ int check_batch(const smol_csum_batch_t* b, const void* d_buf) {
     return SMOL_OK;
 }
 
+// The kernel a batched call runs: its family, variant and (walk / tile / copy kernels) launch shape.
+// One pure function, so that smol_csum_tool_kernel_for names exactly what run() launches.
+enum Family { F_WALK, F_TILE, F_XWALK, F_DWALK, F_STRIPE, F_COPY, F_XCOPY };
+struct Pick {
+    int family;
+    int variant;
+    int shape;
+};
+
+// Variants that serve copy-emit only: copy_kernel (17, 21; 22 / 30 experiments), the transposed
+// layout (49-55, experiments) and the walk kernel's MODE_COPY forms 8 / 11 / 16 (experiments).  Forced
+// on a context, they leave emit / verify / data to the library's choice (the automatic dispatch).
+bool copy_only(int v) { return v == 8 || v == 11 || v == 16 || v == 17 || v == 21 || v == 22 || v == 30 || (v >= 49 && v <= 55); }
+
+Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* b, const KParams& p) {
+    const bool has_desc = b->desc != nullptr;
+    const bool nhc = p.addrs != nullptr;
+    if (mode == MODE_COPY) {  // one fused pass (no tile / deferred variants)
+        // default: variant 21 (csum_copy.hip: variant 17's body chunks = one source load + shift +
+        // sum + store, with the first body round's loads issued ahead of round 1's stores) at its
+        // default shape (16 x 4): C2copy 0.772-0.853 ms (variant 16) -> 0.692 ms (17) -> 0.678 ms
+        // (21; tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 / 17 stay selectable.
+        const int cv = ctx->variant;
+        if (cv >= 49 && cv <= 55 && xcopy_fits(p)) return {F_XCOPY, cv, -1};
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17 || cv == 22 || cv == 30) ? cv : 21;
+        const bool ck = var == 17 || var == 21 || var == 22 || var == 30;
+        const int gv = cv >= 0 ? cv : walk_variant(mode, has_desc);
+        const int shape = ctx->shape >= 0 ? ctx->shape : ck ? (int)CFG_G16U4 : auto_shape(b->len, has_desc, line_grid(gv), gv);
+        return {ck ? F_COPY : F_WALK, var, shape};
+    }
+    int variant = copy_only(ctx->variant) ? -1 : ctx->variant;
+    if (variant < 0) {
+        const int xv = nhc ? 0 : xwalk_auto(mode, b);
+        variant = xv ? xv : auto_variant(mode, has_desc);
+    }
+    if (mode == MODE_EMIT && (b->flags & SMOL_BATCH_FIELD_STORES)) variant = field_store_variant(variant, has_desc);
+    // a kernel that does not serve the batch falls back to the default of its kind (descriptor emit:
+    // the tile kernel; otherwise the walk kernel)
+    const int fallback = (mode == MODE_EMIT && has_desc && !nhc) ? 7 : walk_variant(mode, has_desc);
+    // the stripe kernel (variant 42, experiments): emit / verify of packed fixed-stride 1024-1520-B records
+    if (variant == 42) {
+        if ((mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc && stripe_fits(p)) return {F_STRIPE, 42, -1};
+        variant = fallback;
+    }
+    // the transposed walk (44 / 47 / 57 product, the others experiments): fixed-stride records of
+    // 1024 - 16257 B
+    const int v64 = variant % 64;
+    const bool xw_var = (variant < 64 && (variant == 44 || variant == 47 || variant == 43 || variant == 45 || variant == 46 ||
+                                          variant == 15 || variant == 48 || variant == 57 || variant == 58 || variant == 59)) ||
+                        (variant >= 64 && (v64 == 44 || v64 == 47)) || staged_variant(variant) || (variant >= 82 && variant <= 86);
+    if (xw_var) {
+        if ((mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc && xwalk_fits(p)) return {F_XWALK, variant, -1};
+        variant = fallback;
+    }
+    // descriptor-batch walks: 63 = verify default (cached header windows), 41 = emit default (its emit
+    // form), 60 = the non-temporal-window verify; 56, 60's emit, 61 / 62 (whole field segments) and
+    // 18 / 20 (non-temporal 2-B fields) in the experiments build, which also runs them forced over
+    // fixed-stride batches
+    if (mode == MODE_VERIFY) {
+        if (variant == 41 || variant == 18 || variant == 62) variant = 63;  // emit forms of 63
+        if (variant == 20 || variant % 64 == 61) variant = 60;              // emit forms of 60
+    }
+#ifdef SMOL_EXP
+    const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63 ||
+                        variant == 18 || variant == 20 || variant == 41;
+    const bool dw_ok = (mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc;
+#else
+    const bool dw_var = variant == 60 || variant == 63 || variant == 41;
+    const bool dw_ok = (mode == MODE_VERIFY || (mode == MODE_EMIT && variant != 60)) && has_desc && !nhc;
+#endif
+    if (dw_var) {
+        if (dw_ok) return {F_DWALK, variant, -1};
+        variant = fallback;
+    }
+    // the tile kernel (3 / 4 / 7: nt / plain / nt on the line grid): IP emit and verify only
+    const bool tile_var = variant == 3 || variant == 4 || variant == 7;
+    if (tile_var && (mode == MODE_DATA || nhc)) variant = walk_variant(mode, has_desc);
+    const int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, has_desc, line_grid(variant), variant);
+    if (variant == 3 || variant == 4 || variant == 7) return {F_TILE, variant, shape};
+    return {F_WALK, variant, shape};
+}
+
+const char* family_kernel(const Pick& k) {
+    switch (k.family) {
+        case F_TILE: case F_STRIPE: return "csum_tile_kernel";
+        case F_XWALK: return "xwalk_kernel";
+        case F_DWALK: return "dwalk_kernel";
+        case F_COPY: return "copy_kernel";
+        case F_XCOPY: return "xcopy_kernel";
+        default: return "csum_kernel";
+    }
+}
+
 int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t* b,
         const smol_checksum_caps_t* caps, uint16_t* d_out, uint8_t* d_status, void* stream,
         const uint8_t* d_src = nullptr, const smol_csum_copy_t* d_copy = nullptr,
@@ -263,51 +360,6 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     p.xcd_remap = ctx->xcd_remap >= 0 ? (uint32_t)ctx->xcd_remap : (uint32_t)xcd_remap_auto(mode, b);
     DeviceGuard guard(ctx->device);
     if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
-    // Variants: 0-2, 5-6 = walk kernel (csum_walk.h VarT: load policy, prefetch, chunk
-    // grid), 3-4, 7 = tile kernel (csum_tile.hip: nt / plain loads, nt on the line grid), IP emit
-    // and verify only; 8 = walk kernel without prefetch, copy-emit only (its default; other modes
-    // run variant 0 for it).
-    int variant = ctx->variant;
-    const bool has_desc = b->desc != nullptr;
-    if (variant < 0) {
-        const int xv = d_addrs ? 0 : xwalk_auto(mode, b);
-        variant = xv ? xv : auto_variant(mode, has_desc);
-    }
-    if (mode == MODE_EMIT && (b->flags & SMOL_BATCH_FIELD_STORES)) variant = field_store_variant(variant, has_desc);
-    // the stripe kernel (variant 42) serves emit / verify of packed fixed-stride records of 1024-1520 B
-    // a kernel that does not serve the batch falls back to the default of its kind (descriptor emit:
-    // the tile kernel; otherwise the walk kernel)
-    const int fallback = (mode == MODE_EMIT && has_desc && !d_addrs) ? 7 : walk_variant(mode, has_desc);
-    const bool stripe = variant == 42 && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && stripe_fits(p);
-    if (variant == 42 && !stripe) variant = fallback;
-    // the transposed walk (variants 44 / 47, 64 + 44 / 47): fixed-stride records of 1024 - 16257 B
-    const bool xw_var = variant % 64 == 44 || variant % 64 == 47 || variant == 43 || variant == 45 || variant == 46 || variant == 15 ||
-                        variant == 48 || variant == 57 ||
-                        variant == 58 || variant == 59;
-    const bool xwalk = xw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs && xwalk_fits(p);
-    if (xw_var && !xwalk) variant = fallback;
-    if (variant == 41 && mode == MODE_VERIFY) variant = 63;  // 41: the emit form of 63
-    // descriptor-batch walks: 63 = verify default (cached header windows), 41 = emit default, 60 = its
-    // non-temporal-window verify; 56, 60's emit and 61 / 62 (emit with whole field segments) in the
-    // experiments build only
-#ifdef SMOL_EXP
-    const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63 ||
-                        variant == 18 || variant == 20 || variant == 41;
-    if (variant == 18 && mode == MODE_VERIFY) variant = 63;  // emit forms of 63 / 60
-    if (variant == 20 && mode == MODE_VERIFY) variant = 60;
-    if (variant % 64 == 61 && mode == MODE_VERIFY) variant = 60;  // an emit form of 60
-    if (variant == 62 && mode == MODE_VERIFY) variant = 63;      // an emit form of 63
-    // (forced, the experiments build also runs it over fixed-stride batches)
-    const bool dwalk = dw_var && (mode == MODE_EMIT || mode == MODE_VERIFY) && !d_addrs;
-#else
-    const bool dw_var = variant == 60 || variant == 63 || variant == 41;
-    const bool dwalk = dw_var && (mode == MODE_VERIFY || (mode == MODE_EMIT && variant != 60)) && has_desc && !d_addrs;
-#endif
-    if (dw_var && !dwalk) variant = fallback;
-    const bool tile_var = variant == 3 || variant == 4 || variant == 7;  // tile kernel: nt / plain / nt line grid
-    if (tile_var && (mode == MODE_DATA || mode == MODE_COPY || d_addrs)) variant = walk_variant(mode, has_desc);
-    const bool use_tile = variant == 3 || variant == 4 || variant == 7;
-    int shape = ctx->shape >= 0 ? ctx->shape : auto_shape(b->len, has_desc, line_grid(variant), variant);
     const hipStream_t s = (hipStream_t)stream;
     // A batch larger than launch_records records goes out as consecutive launches on the stream,
     // each over the next launch_records records (the per-record arrays advance with them).
@@ -328,45 +380,45 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         }
         return SMOL_OK;
     }
-    if (mode == MODE_COPY) {  // one fused pass; the walk kernel only (no tile / deferred variants)
-        // default: variant 21 (csum_copy.hip: variant 17's body chunks = one source load + shift +
-        // sum + store, with the first body round's loads issued ahead of round 1's stores) at its
-        // default shape (16 x 4): C2copy 0.772-0.853 ms (variant 16) -> 0.692 ms (17) -> 0.678 ms
-        // (21; tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 / 17 stay selectable.
-        const int cv = ctx->variant;
-        if (cv >= 49 && cv <= 55 && xcopy_fits(p)) {  // the transposed layout (experiments build)
-            hipError_t e = launch_xcopy(cv, p, s);
-            if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
-            return SMOL_OK;
+    const Pick k = pick_kernel(ctx, mode, b, p);
+    if (k.family == F_XWALK && mode == MODE_EMIT && staged_variant(k.variant)) {
+        // staged emit: the field entries of kStageChunk records at a time (scratch owned by the context),
+        // each chunk's staging launch followed by its segment pass
+        const uint64_t want = b->n < kStageChunk ? b->n : kStageChunk;
+        if (ctx->stage_cap < want) {
+            if (ctx->stage) (void)hipFree(ctx->stage);
+            ctx->stage = nullptr;
+            ctx->stage_cap = 0;
+            hipError_t ea = hipMalloc(&ctx->stage, want * sizeof(uint64_t));
+            if (ea != hipSuccess) {
+                ctx->stage = nullptr;
+                return hip_fail(ea, "hipMalloc (staged emit entries)");
+            }
+            ctx->stage_cap = want;
         }
-        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17 || cv == 22 || cv == 30) ? cv : 21;
-        const int cshape = ctx->shape >= 0 ? ctx->shape : ((var == 17 || var == 21) ? (int)CFG_G16U4 : shape);
-        hipError_t e = launch_csum(MODE_COPY, cshape, var, p, ctx->max_blocks, s);
-        if (e != hipSuccess) return hip_fail(e, "copy-emit kernel launch");
+        for (uint64_t i0 = 0; i0 < b->n; i0 += kStageChunk) {
+            KParams q = p;
+            q.n = b->n - i0 < kStageChunk ? b->n - i0 : kStageChunk;
+            q.buf = d_buf + i0 * b->stride;
+            if (d_status) q.status = d_status + i0;
+            q.stage = ctx->stage;
+            const hipError_t e = launch_xwalk(mode, k.variant, q, s);
+            if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
+        }
         return SMOL_OK;
     }
-    if (dwalk) {
-        hipError_t e = launch_dwalk(mode, variant, p, s);
-        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
-        return SMOL_OK;
+    hipError_t e = hipSuccess;
+    switch (k.family) {
+        case F_XCOPY: e = launch_xcopy(k.variant, p, s); break;
+        case F_DWALK: e = launch_dwalk(mode, k.variant, p, s); break;
+        case F_XWALK: e = launch_xwalk(mode, k.variant, p, s); break;
+        case F_STRIPE: e = launch_stripe(mode, p, s); break;
+        case F_TILE:
+            e = launch_tile(mode, k.shape, k.variant == 7 ? 2 : k.variant - 3, ctx->tile_records, p, ctx->max_blocks, s);
+            break;
+        default: e = launch_csum(mode, k.shape, k.variant, p, ctx->max_blocks, s); break;  // walk / copy kernels
     }
-    if (xwalk) {
-        hipError_t e = launch_xwalk(mode, variant, p, s);
-        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
-        return SMOL_OK;
-    }
-    if (stripe) {
-        hipError_t e = launch_stripe(mode, p, s);
-        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
-        return SMOL_OK;
-    }
-    if (use_tile) {
-        hipError_t e = launch_tile(mode, shape, variant == 7 ? 2 : variant - 3, ctx->tile_records, p, ctx->max_blocks, s);
-        if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
-        return SMOL_OK;
-    }
-    hipError_t e = launch_csum(mode, shape, variant, p, ctx->max_blocks, s);
-    if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
+    if (e != hipSuccess) return hip_fail(e, mode == MODE_COPY ? "copy-emit kernel launch" : "checksum kernel launch");
     return SMOL_OK;
 }
 
@@ -410,6 +462,8 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     c->max_blocks_set = false;
     c->xcd_remap = -1;
     c->launch_records = 0;
+    c->stage = nullptr;
+    c->stage_cap = 0;
     c->device = device;
     c->num_cu = cus;
     c->max_blocks = kNaturalGrid;
@@ -424,6 +478,7 @@ int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
     {
         DeviceGuard guard(ctx->device);
         (void)hipFree(ctx->dummy);
+        if (ctx->stage) (void)hipFree(ctx->stage);
     }
     delete ctx;
     return SMOL_OK;
@@ -635,6 +690,18 @@ int smol_csum_tool_field_probe_list(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64
     return e == hipSuccess ? SMOL_OK : hip_fail(e, "field-probe kernel launch");
 }
 
+int smol_csum_tool_segment_probe(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint32_t* d_bitmap, int flags,
+                                 void* stream) {
+    if (!ctx || !d_buf || !d_bitmap || (bytes & 15u) || ((uintptr_t)d_buf & 15u) || ((uintptr_t)d_bitmap & 15u) ||
+        (flags & ~1))
+        return SMOL_EINVAL;
+    DeviceGuard guard(ctx->device);
+    if (!guard.ok) return hip_fail(hipErrorInvalidDevice, "hipSetDevice");
+    hipError_t e = launch_segment_probe(d_buf, bytes, d_bitmap, flags & 1, (uint32_t)(ctx->num_cu > 0 ? ctx->num_cu : 256) * 8u,
+                                        (hipStream_t)stream);
+    return e == hipSuccess ? SMOL_OK : hip_fail(e, "segment-probe kernel launch");
+}
+
 int smol_csum_tool_field_scatter(smol_csum_ctx_t* ctx, uint8_t* d_buf, uint64_t bytes, const uint64_t* d_addrs,
                                  const uint16_t* d_vals, uint64_t n, int flags, void* stream) {
     if (!ctx || !d_buf || (n && (!d_addrs || !d_vals)) || (flags & ~15) || n > (0xFFFFFFull << 8)) return SMOL_EINVAL;
@@ -652,16 +719,27 @@ int smol_csum_tool_auto_shape(uint32_t len, int has_desc) {
 }
 
 const char* smol_csum_tool_kernel_name(const smol_csum_ctx_t* ctx, int op, int has_desc) {
+    // Without the batch this cannot see its record length: it answers for a batch that no
+    // length-dependent kernel serves (descriptor batches exactly; fixed-stride batches the walk kernel's
+    // lengths).  smol_csum_tool_kernel_for takes the batch.
     if (!ctx || op < MODE_DATA || op > MODE_COPY) return "";
-    if (op == MODE_COPY) {
-        const int cv = ctx->variant;
-        return (cv == 1 || cv == 8 || cv == 11 || cv == 16) ? "csum_kernel" : "copy_kernel";
-    }
-    const int v = ctx->variant >= 0 ? ctx->variant : auto_variant(op, has_desc != 0);
-    if (has_desc && ((v == 60 && op == MODE_VERIFY) || ((v == 63 || v == 41) && (op == MODE_VERIFY || op == MODE_EMIT))))
-        return "dwalk_kernel";
-    const bool tile = (v == 3 || v == 4 || v == 7) && (op == MODE_EMIT || op == MODE_VERIFY);
-    return tile ? "csum_tile_kernel" : "csum_kernel";
+    smol_csum_batch_t b;
+    std::memset(&b, 0, sizeof b);
+    b.n = 1;
+    b.len = b.stride = 64;
+    b.desc = has_desc ? reinterpret_cast<const smol_csum_desc_t*>(ctx->dummy) : nullptr;
+    return smol_csum_tool_kernel_for(ctx, op, &b);
+}
+
+const char* smol_csum_tool_kernel_for(const smol_csum_ctx_t* ctx, int op, const smol_csum_batch_t* b) {
+    if (!ctx || !b || op < MODE_DATA || op > MODE_COPY) return "";
+    KParams p;
+    std::memset(&p, 0, sizeof p);
+    p.desc = b->desc;
+    p.n = b->n;
+    p.stride = b->stride;
+    p.len = b->len;
+    return family_kernel(pick_kernel(ctx, op, b, p));
 }
 
 uint32_t smol_csum_tool_last_launch(void) { return g_last_launch.load(std::memory_order_relaxed); }

@@ -53,6 +53,7 @@ struct KParams {
     const uint8_t* addrs;  // 6LoWPAN NHC UDP batches: 32 B (IPv6 src, dst) per record, else nullptr
     uint32_t xcd_remap;    // walk kernel: 0 dispatch order; 1 block b takes the records of block
                            // xcd_block(b); K >= 2: those of xcd_chunk(b, K) (see below)
+    uint64_t* stage;       // staged emit (csum_xwalk.hip variant 80): one 8-B field entry per record
 };
 
 // The 8 XCDs of an MI355X are dealt workgroups round-robin (MI355X_MICROARCH.md, workgroup dispatch:
@@ -130,6 +131,10 @@ bool xcopy_fits(const KParams& p);
 hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s);
 hipError_t launch_xcopy(int variant, const KParams& p, hipStream_t s);
 hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s);
+// Staged emit (variants 80 / 81): the transposed walk writes each record's field entry to p.stage, then
+// the segment pass writes the field segments whole (csum_xwalk.hip).  Records per launch pair:
+constexpr uint64_t kStageChunk = 1ull << 21;
+inline bool staged_variant(int v) { return v == 80 || v == 81; }
 
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
 struct SynthParams {
@@ -154,5 +159,7 @@ hipError_t launch_field_scatter(uint8_t* buf, uint64_t bytes, const uint64_t* ad
                                 int nt, hipStream_t s);
 hipError_t launch_field_probe_list(uint8_t* buf, uint64_t bytes, const uint64_t* addrs, const uint32_t* first,
                                    int seg64, uint32_t max_blocks, hipStream_t s);
+hipError_t launch_segment_probe(uint8_t* buf, uint64_t bytes, const uint32_t* bitmap, int nt, uint32_t max_blocks,
+                                hipStream_t s);
 
 }  // namespace smolcsum

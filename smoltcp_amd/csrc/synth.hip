@@ -396,6 +396,56 @@ hipError_t launch_field_scatter(uint8_t* buf, uint64_t bytes, const uint64_t* ad
     return hipGetLastError();
 }
 
+// Emit's floor in emit's own store shape (round 6): the read-only stream above over the buffer, and
+// every 64-B segment that holds a checksum field written back whole, with the bytes just read (nothing
+// changes), by the lanes that loaded it, right after the piece's loads.  bitmap: one bit per 64-B
+// segment of the buffer (bit s % 32 of word s / 32), set for the segments emit writes.  An 8-KiB piece
+// is 128 segments = 4 bitmap words, read as one uniform (scalar) load; lane l's chunk of load u lies
+// in segment 16 u + l / 4 of the piece.  nt: the segments stored non-temporal (emit's form for packed
+// 1400-1580-B records, csum_api.cpp xwalk_auto).  The tail past the last whole piece is read, not
+// written.
+template <bool NT>
+__global__ __launch_bounds__(256) void segment_probe_kernel(uint8_t* buf, uint64_t n16, const uint32_t* bitmap) {
+    constexpr int UNR = 8;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const uint64_t per = 64ull * UNR;
+    const u32x4s* q = reinterpret_cast<const u32x4s*>(buf);
+    typedef __attribute__((address_space(1))) u32x4s* gv4;
+    uint32_t acc = 0;
+    for (uint64_t base = w0 * per; base + per <= n16; base += nw * per) {
+        u32x4s v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) v[u] = __builtin_nontemporal_load(q + base + u * 64 + lane);
+        const uint64_t piece = base / per;
+        uint32_t bits[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bits[k] = bitmap[4 * piece + k];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            acc += __builtin_amdgcn_sad_u16(v[u].x, 0, 0) + __builtin_amdgcn_sad_u16(v[u].w, 0, 0);
+            if ((bits[u >> 1] >> (16 * (u & 1) + lane / 4)) & 1u) {
+                u32x4s x = v[u];
+                asm volatile("" : "+v"(x));  // opaque: the stored values are the ones just read
+                if constexpr (NT) __builtin_nontemporal_store(x, (gv4)buf + base + u * 64 + lane);
+                else ((gv4)buf)[base + u * 64 + lane] = x;
+            }
+        }
+    }
+    const uint64_t tail = n16 / per * per;
+    for (uint64_t i = tail + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+        acc += q[i].x;
+    asm volatile("" ::"v"(acc));  // keeps every load live
+}
+
+hipError_t launch_segment_probe(uint8_t* buf, uint64_t bytes, const uint32_t* bitmap, int nt, uint32_t max_blocks,
+                                hipStream_t s) {
+    if (nt) hipLaunchKernelGGL((segment_probe_kernel<true>), dim3(max_blocks), dim3(256), 0, s, buf, bytes / 16, bitmap);
+    else hipLaunchKernelGGL((segment_probe_kernel<false>), dim3(max_blocks), dim3(256), 0, s, buf, bytes / 16, bitmap);
+    return hipGetLastError();
+}
+
 hipError_t launch_field_probe(uint8_t* buf, uint64_t bytes, uint64_t stride, uint32_t f1, uint32_t f2,
                               uint32_t max_blocks, hipStream_t s) {
     hipLaunchKernelGGL(field_probe_kernel, dim3(max_blocks), dim3(256), 0, s, buf, bytes / 16, stride, f1, f2);

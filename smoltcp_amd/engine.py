@@ -122,6 +122,21 @@ def _caps(caps) -> Caps:
     return c
 
 
+def segment_bitmap(addrs, nbytes: int):
+    """The segment probe's bitmap for 2-byte fields at the byte offsets `addrs` (device int64 tensor) of
+    an `nbytes` buffer: bit s set for every 64-B segment s holding a field byte, ceil(nbytes / 8192) * 4
+    int32 words (whole 8-KiB pieces of 128 segments)."""
+    import torch
+
+    nseg = (nbytes + 8191) // 8192 * 128
+    flags = torch.zeros(nseg, dtype=torch.int64, device=addrs.device)
+    flags[addrs >> 6] = 1
+    flags[(addrs + 1) >> 6] = 1
+    words = (flags.view(-1, 32) << torch.arange(32, device=addrs.device, dtype=torch.int64)).sum(dim=1)
+    words = torch.where(words >= 1 << 31, words - (1 << 32), words)
+    return words.to(torch.int32).contiguous(), int(flags.sum().item())
+
+
 class ChecksumEngine:
     """One device context.  Not thread-safe: use one engine per host thread."""
 
@@ -307,6 +322,15 @@ class ChecksumEngine:
                                                     self._stream(stream)),
               "smol_csum_tool_field_probe_list")
 
+    def segment_probe(self, buf, bitmap, nt: bool = False, stream=None):
+        """Emit's floor in its store shape (tooling, smol_csum_tool_segment_probe): the read stream over
+        `buf` plus every 64-B segment whose bit is set in `bitmap` (device int32 tensor, one bit per
+        segment, see segment_bitmap) rewritten whole with its own bytes; `nt`: non-temporal stores."""
+        nbytes = buf.numel() // 16 * 16
+        check(self._L.smol_csum_tool_segment_probe(self._h, buf.data_ptr(), nbytes, bitmap.data_ptr(), int(bool(nt)),
+                                                 self._stream(stream)),
+              "smol_csum_tool_segment_probe")
+
     def field_scatter(self, buf, addrs, vals, nt: int = 0, stream=None):
         """A separate store pass (tooling, smol_csum_tool_field_scatter): the big-endian u16 `vals[i]`
         at byte offset `addrs[i]` (device int64 / uint16-as-int16 tensors) of `buf`.  `nt`: the flags
@@ -326,9 +350,17 @@ class ChecksumEngine:
         check(self._L.smol_csum_tool_set_tile(self._h, int(records)), "smol_csum_tool_set_tile")
 
     def kernel_name(self, op: str, has_desc: bool = False) -> str:
-        """The kernel an IP-path `op` ("data", "emit", "verify", "copy_emit") launches here."""
+        """Deprecated: the kernel an IP-path `op` launches for a batch of short records (no record
+        length is passed; see kernel_for)."""
         code = {"data": 0, "emit": 1, "verify": 2, "copy_emit": 3}[op]
         return self._L.smol_csum_tool_kernel_name(self._h, code, int(bool(has_desc))).decode()
+
+    def kernel_for(self, op: str, batch: Batch) -> str:
+        """The kernel (rocprofv3 name prefix) an IP-path `op` ("data", "emit", "verify", "copy_emit")
+        launches for `batch` with this engine's settings: the library's own dispatch decision."""
+        code = {"data": 0, "emit": 1, "verify": 2, "copy_emit": 3}[op]
+        b = batch.c()
+        return self._L.smol_csum_tool_kernel_for(self._h, code, ctypes.byref(b)).decode()
 
     def variant_built(self, variant: int) -> bool:
         """Whether this build of the library runs `variant` (the product library: the defaults and

@@ -88,7 +88,11 @@ def test_bench_gpu_contract():
     rl = d["roofline"]
     assert rl["bound"] == "hbm" and rl["unit"] == "GB/s" and rl["peak"] == 8000.0
     assert 0 < rl["frac"] < 1 and abs(rl["achieved"] / rl["peak"] - rl["frac"]) < 1e-3
-    assert rl["floor"]["kernel"] == "field_probe_kernel" and 0 < rl["floor_frac"]
+    assert rl["floor"]["kernel"] == "segment_probe_kernel" and 0 < rl["floor_frac"]
+    assert rl["floor"]["segments"] == 1310720 * d["config"]["records_per_gpu"] // (1 << 20)  # C2: 1.25 per record
+    assert rl["floor_2b"]["kernel"] == "field_probe_kernel" and 0 < rl["floor_2b_frac"]
+    sp = d["parity_sample"]["spread"]  # the oracle over runs of records spread across the whole batch
+    assert sp["emit_bitexact"] and sp["verify_bitexact"] and sp["records"] >= 65536
     assert 0 < rl["read_only_frac"] and 0 < rl["step_frac"] < 1
     assert rl["step_algorithmic_bytes"] == sum(k["algorithmic_bytes_per_launch"] for k in d["kernels_roofline"].values())
     n64 = d["config"]["records_per_gpu"] // 64  # 1/64 single-bit flips (a few the gates cannot see)

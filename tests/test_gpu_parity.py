@@ -743,6 +743,8 @@ WIDE_KERNELS = {
     46: ("xwalk_kernel", 16257),
     47: ("xwalk_kernel", 16257),
     57: ("xwalk_kernel", 16257),
+    80: ("xwalk_kernel", 16257),  # staged emit: field entries, then the segment pass (round 6)
+    81: ("xwalk_kernel", 16257),
     48: ("xwalk_kernel", 16257),
     59: ("xwalk_kernel", 16257),
 }
@@ -811,6 +813,42 @@ def test_wide_record_kernels(eng, variant):
         finally:
             eng.set_variant(-1)
         assert np.array_equal(st, oracle.batch_verify(host, None, n, stride, L, E.KIND_IP, CAPS_DEFAULT))
+
+
+@pytest.mark.parametrize("variant", [80, 81])
+def test_staged_emit_chunks(eng, variant):
+    """The staged emit over more records than one staging chunk (kStageChunk = 2^21: several staging
+    launch + segment pass pairs, the context's entry buffer grown from a small first batch) writes the
+    same bytes as the transposed walk's in-place emit (variant 57, oracle-checked by the tests above), and
+    the oracle agrees on runs of records at the chunk seams."""
+    eng.need(variant)
+    L, n = 1024, (1 << 21) * 2 + 37
+    b = E.Batch.fixed(n, L, L, E.KIND_IP)
+    buf = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+    eng.synth(buf, b, E.SYNTH_UDP4, seed=99)
+    small = E.Batch.fixed(100, L, L, E.KIND_IP)
+    ref = buf.clone()
+    eng.set_variant(57)
+    try:
+        eng.emit(ref, b)
+    finally:
+        eng.set_variant(-1)
+    got = buf.clone()
+    eng.set_variant(variant)
+    try:
+        eng.emit(got[: 100 * L + 64].clone(), small)  # the entry buffer first sized for 100 records
+        eng.emit(got, b)
+        assert (eng.last_launch()["kernel"], eng.last_launch()["variant"]) == ("xwalk_kernel", variant)
+    finally:
+        eng.set_variant(-1)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    host = buf.cpu().numpy()
+    for lo in (0, (1 << 21) - 40, (1 << 22) - 40, n - 60):
+        hi = min(n, lo + 80)
+        want = host[lo * L: hi * L].copy()
+        oracle.batch_emit(want, None, hi - lo, L, L, E.KIND_IP, CAPS_DEFAULT)
+        assert np.array_equal(got[lo * L: hi * L].cpu().numpy(), want), lo
 
 
 def _wide_case(eng, variant, kname, host, off, n, L, kind, caps, stride=None):

@@ -112,3 +112,77 @@ def test_last_launch_families(eng):
     eng.copy_emit(buf, b, src, cp)
     ll = eng.last_launch()
     assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("copy_kernel", 21, 16, 4), ll
+
+
+def test_kernel_for_names_the_launch(eng):
+    """smol_csum_tool_kernel_for (csum_api.cpp pick_kernel, the decision run() launches) names the kernel
+    every fixed-stride length, descriptor batch and forced variant actually ran (last_launch)."""
+    cases = [(LL, stride, op) for LL, stride in ((1320, 1320), (1500, 1500), (1500, 1564), (1600, 1600), (2500, 2500),
+                                                 (9000, 9000), (12000, 12000), (1024, 1024), (1700, 1764))
+             for op in ("emit", "verify", "data")]
+    for LL, stride, op in cases:
+        bb = E.Batch.fixed(8, stride, LL, E.KIND_IP)
+        t = torch.zeros(8 * stride + 64, dtype=torch.uint8, device="cuda:0")
+        want = eng.kernel_for(op, bb)
+        getattr(eng, op)(t, bb)
+        assert eng.last_launch()["kernel"] == want, (LL, stride, op, want, eng.last_launch())
+    n, L = 64, 1500
+    buf = torch.zeros(n * L, dtype=torch.uint8, device="cuda:0")
+    bd = E.Batch.from_records(np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32), E.KIND_IP, "cuda:0")
+    for v in (-1, 7, 13, 60, 63, 41):
+        eng.set_variant(v)
+        try:
+            for op in ("emit", "verify"):
+                want = eng.kernel_for(op, bd)
+                getattr(eng, op)(buf, bd)
+                assert eng.last_launch()["kernel"] == want, (v, op, want, eng.last_launch())
+        finally:
+            eng.set_variant(-1)
+
+
+@pytest.mark.parametrize("v", [17, 21])
+def test_forced_copy_variant_serves_other_ops(eng, v):
+    """A copy-emit-only variant forced on the context (it used to fail emit / verify with
+    SMOL_EHIP) runs copy-emit itself and leaves emit / verify on their default kernels, bit-exact."""
+    import oracle
+
+    n, L = 96, 1500
+    b = E.Batch.fixed(n, L, L, E.KIND_IP)
+    buf = torch.zeros(n * L, dtype=torch.uint8, device="cuda:0")
+    eng.synth(buf, b, E.SYNTH_UDP4, seed=11)
+    host = buf.cpu().numpy().copy()
+    want_emit, want_verify = eng.kernel_for("emit", b), eng.kernel_for("verify", b)
+    eng.set_variant(v)
+    try:
+        assert eng.kernel_for("emit", b) == want_emit and eng.kernel_for("verify", b) == want_verify
+        eng.emit(buf, b)
+        assert eng.last_launch()["kernel"] == want_emit
+        st = eng.verify(buf, b)
+        assert eng.last_launch()["kernel"] == want_verify
+        src = torch.randint(0, 256, (n * 1472 + 16,), dtype=torch.uint8, device="cuda:0")
+        cp = torch.from_numpy(E.make_copies(np.arange(n, dtype=np.uint64) * 1472, 28, 1472).view(np.uint8).copy()).cuda()
+        eng.copy_emit(torch.zeros_like(buf), b, src, cp)
+        ll = eng.last_launch()
+        assert (ll["kernel"], ll["variant"]) == ("copy_kernel", v), ll
+    finally:
+        eng.set_variant(-1)
+    ref = host.copy()
+    oracle.batch_emit(ref, None, n, L, L, E.KIND_IP, (0, 0, 0, 0, 0))
+    assert np.array_equal(buf.cpu().numpy(), ref)
+    assert np.array_equal(st.cpu().numpy(), oracle.batch_verify(ref, None, n, L, L, E.KIND_IP, (0, 0, 0, 0, 0)))
+
+
+@pytest.mark.parametrize("nt", [False, True])
+def test_segment_probe_changes_nothing(eng, nt):
+    """The segment-shape floor probe (bench.py roofline.floor) rewrites the field segments with their own
+    bytes: the buffer is bit-identical afterwards, for C2-like field offsets and a partial last piece."""
+    n, L = 3000, 1500
+    nbytes = n * L + 5000  # a tail past the last whole 8-KiB piece
+    host = np.random.default_rng(8).integers(0, 256, nbytes, dtype=np.uint8)
+    d = torch.from_numpy(host.copy()).cuda()
+    addrs = torch.from_numpy(np.sort(np.concatenate([np.arange(n) * L + 10, np.arange(n) * L + 26])).astype(np.int64)).cuda()
+    bitmap, nseg = E.segment_bitmap(addrs, nbytes // 16 * 16)
+    assert nseg == len({a >> 6 for a in addrs.cpu().tolist()} | {(a + 1) >> 6 for a in addrs.cpu().tolist()})
+    eng.segment_probe(d, bitmap, nt=nt)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), host)
