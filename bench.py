@@ -65,6 +65,9 @@ def parse_args(argv=None):
     ap.add_argument("--xcd-remap", type=int, default=-1, help="1/0: force the XCD-contiguous block order (tuning; "
                                                                "-1: the library's choice)")
     ap.add_argument("--launch-records", type=int, default=-1, help="records per kernel launch (tuning; 0: all)")
+    ap.add_argument("--src-stride", type=int, default=1472,
+                    help="c2copy: bytes between consecutive payloads in the source buffer (1472: packed; an "
+                         "experiment knob: 1536 puts every payload on its own 128-B lines)")
     ap.add_argument("--batches", type=int, default=4,
                     help="TX / RX batch pairs the steps take in turn (1: re-emit one batch; C5 always 1: its one "
                          "201-GB buffer is emitted and verified in place)")
@@ -128,7 +131,7 @@ def launch_ranks(args, argv) -> int:
 class Workload:
     """Two HBM batches (tx, rx) of one config, generated on the device."""
 
-    def __init__(self, E, eng, cfg: str, n: int, rank: int, dev, batches: int = 1):
+    def __init__(self, E, eng, cfg: str, n: int, rank: int, dev, batches: int = 1, src_stride: int = 1472):
         import torch
 
         self.cfg = cfg
@@ -178,8 +181,8 @@ class Workload:
         eng.synth(self.tx, self.batch, self.profile, seed)
         if cfg == "c2copy":
             # payloads live in a socket-buffer-like source, back to back; headers are in the records
-            self.src = torch.randint(0, 256, (self.n * 1472 + 16,), dtype=torch.uint8, device=dev)
-            cp = E.make_copies(np.arange(self.n, dtype=np.uint64) * 1472, 28, 1472)
+            self.src = torch.randint(0, 256, (self.n * src_stride + 16,), dtype=torch.uint8, device=dev)
+            cp = E.make_copies(np.arange(self.n, dtype=np.uint64) * src_stride, 28, 1472)
             self.copy = torch.from_numpy(cp.view(np.uint8).copy()).to(dev)
             self.read_bytes = self.n * (28 + 1472)   # headers from the record, payload from the source
             self.write_bytes_tx = self.n * (1472 + 4)
@@ -650,7 +653,7 @@ def main(argv=None):
     eng.set_xcd_remap(args.xcd_remap)
     if args.launch_records >= 0:
         eng.set_launch_records(args.launch_records)
-    wl = Workload(E, eng, args.config, args.n, rank, dev, args.batches)
+    wl = Workload(E, eng, args.config, args.n, rank, dev, args.batches, args.src_stride)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
@@ -806,7 +809,8 @@ def main(argv=None):
     if wl.copy is not None and rank == 0:
         # the unfused TX path for comparison: payload copy (strided device copy) then emit
         dst = wl.tx.view(wl.n, 1500)[:, 28:]
-        srcv = wl.src[: wl.n * 1472].view(wl.n, 1472)
+        sst = args.src_stride
+        srcv = wl.src[: wl.n * sst].view(wl.n, sst)[:, :1472]
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(2):
             dst.copy_(srcv)

@@ -123,35 +123,27 @@ int auto_variant(int mode, bool has_desc) {
     return walk_variant(mode, has_desc);
 }
 
-// Round 5: the transposed walk (csum_xwalk.hip, variant 47: emit with whole field segments) for
-// fixed-stride records where it beats the walk kernel.  Verify / emit of synthetic IPv4/UDP over
-// ~1.5 GB, R = 4 batches in turn, one box per file (tools/exp_r05_vlen.py, profiles/r05_experiments/
-// xwalk_vs_walk_packed.jsonl, xwalk_vs_walk_gap64.jsonl, xwalk_verify_fine.jsonl,
-// xwalk_line_aligned.jsonl), walk / transposed walk time, packed:
-//   length   1024 1320 1472 1500 1536 1600 1700 1792 1921 2048 2500 3969 4096 5000 8065 8192 9000 12000
-//   verify   0.89 0.96 1.00 1.03 0.98 1.00 1.78 1.55 1.55 2.27 2.27 1.51 1.26 1.50 1.04 0.93 1.05  0.99
-//   emit     1.01 0.96 0.97 0.94 0.97 0.96 1.68 1.54 1.53 2.12 2.10 1.44 1.15 1.39 1.01 0.94 1.08  1.00
-// verify 1473-1665 B (every 20-50 B): 1.02-1.04 except 1536 (0.98) and 1600 (1.00); with 64-B gaps
-// verify 0.91 (1024) 0.92 (1320) 1.00 (1500) 1.72 (1700) 2.22 (2500) 1.49 (5000) 1.06 (9000) 1.00
-// (12000), emit within 2 % of that.  The walk kernel's shapes leave lanes idle from 1666 B (8 x 7
-// x 2 chunks no longer hold a record) and fit whole 128-B lines exactly at multiples of 128 B; past
-// 8065 B the transposed walk takes one record per wavefront and the two trade places by length.
-//
-// Variant 57 (47 with the field segments stored non-temporal) for emit of packed 1400-1580-B
-// records, not multiples of 64 B.  Emit in bench.py's step order (emit of TX batch i, then the
-// default verify of RX batch i, R = 4; tools/exp_r05_vlen.py STEP=1,
-// profiles/r05_experiments/xwalk_cached_first_kib.txt, xwalk_nt_segments_step.txt), walk 39 / 45
-// (47 with each record's first KiB loaded cached) / 57, ms: IPv4/UDP 1400 0.319 / 0.319 / 0.315,
-// 1500 0.319 / 0.320 / 0.316, 1536 0.291 / 0.291 / 0.309, 1600 0.290 / 0.310 / 0.313; C2 in bench.py
-// 0.3214 (39) -> 0.3124 (45) -> 0.3084 ms (57), 5318 -> 5400 -> 5449 GiB/s.  C4's IPv6 mix at 1320 B
-// (outside the range): 57 0.273 against walk 39's 0.271 ms; 45 lost 1.7 % on it at 1500 B.
-// Returns the transposed-walk variant to run (0: none).
+// The transposed walk (csum_xwalk.hip) for fixed-stride records where it beats the walk kernel, from a
+// measured table (round 6; VERDICT r05 item 7 replaced round 5's fitted length windows): one length
+// sweep, tools/sweep_dispatch.py, over 1024 .. 9023 B in steps of 64 B (multiples of 64, + 28, and + 28
+// with 64-B gaps), verify and emit (emit in bench.py's step order), on three boxes
+// (profiles/r06_dispatch_sweep_box{1,2,3}.jsonl), turned into dispatch_table.inc by
+// tools/gen_dispatch_table.py (the least summed time per entry).  Verify: the walk kernel (5), the
+// transposed walk (47) or 47 with the first-load hint (89: lanes 0-3 of each record's first instruction
+// with the default cache policy; C2 verify 0.2342 -> 0.2259 ms); emit: the walk kernel (39), 47 or 57 (47
+// with non-temporal field segments).  Outside 1024 .. 9023 B the walk kernel (round 5: past 9000 B the
+// two trade places by length, within 2 %).
+// Returns the transposed-walk variant to run (0: the walk kernel).
+#include "dispatch_table.inc"
+
 int xwalk_auto(int mode, const smol_csum_batch_t* b) {
     if (b->desc || b->stride < b->len || (mode != MODE_VERIFY && mode != MODE_EMIT)) return 0;
-    const bool packed = b->stride == b->len;
-    if (b->len >= 1666) return b->len <= 8065 ? 47 : 0;
-    if (mode == MODE_EMIT) return packed && b->len >= 1400 && b->len <= 1580 && b->len % 64 != 0 ? 57 : 0;
-    return packed && b->len >= 1473 && b->len % 128 != 0 ? 47 : 0;
+    if (b->len < 1024 || b->len >= 1024 + 64 * 125) return 0;
+    const uint32_t k = (b->len - 1024) / 64;
+    const int col = b->stride != b->len ? 2 : (b->len % 64 == 0 ? 0 : 1);
+    const char c = (mode == MODE_VERIFY ? kVerifyTable : kEmitTable)[k][col];
+    if (mode == MODE_VERIFY) return c == 'h' ? 89 : c == 'x' ? 47 : 0;
+    return c == 'n' ? 57 : c == 'x' ? 47 : 0;
 }
 
 // The XCD block order (csum_launch.h xcd_block / xcd_chunk) when none is forced: the contiguous order
@@ -174,11 +166,11 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
-    if (variant == 47 || variant == 57 || variant == 45 || (variant >= 80 && variant <= 86)) return 44;
+    if (variant == 47 || variant == 57 || variant == 45 || (variant >= 80 && variant <= 92)) return 44;
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62 || variant == 18) return 63;  // (63 stores 2-B fields only)
     if (variant == 20) return 60;
-    if (variant == 41) return 41;
+    if (variant == 41 || variant == 94) return 41;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
@@ -190,11 +182,11 @@ int field_store_variant(int variant, bool has_desc) {
 bool variant_built(int v) {
     switch (v) {
         case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 41: case 44: case 47: case 57: case 60: case 63:
-            return true;
+        case 89: case 94: return true;
         default: break;
     }
 #ifdef SMOL_EXP
-    if (v >= 80 && v <= 86) return true;
+    if ((v >= 80 && v <= 88) || v == 90 || v == 91 || v == 92) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -287,7 +279,7 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     const int v64 = variant % 64;
     const bool xw_var = (variant < 64 && (variant == 44 || variant == 47 || variant == 43 || variant == 45 || variant == 46 ||
                                           variant == 15 || variant == 48 || variant == 57 || variant == 58 || variant == 59)) ||
-                        (variant >= 64 && (v64 == 44 || v64 == 47)) || staged_variant(variant) || (variant >= 82 && variant <= 86);
+                        (variant >= 64 && (v64 == 44 || v64 == 47)) || staged_variant(variant) || (variant >= 82 && variant <= 92);
     if (xw_var) {
         if ((mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc && xwalk_fits(p)) return {F_XWALK, variant, -1};
         variant = fallback;
@@ -297,15 +289,15 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     // 18 / 20 (non-temporal 2-B fields) in the experiments build, which also runs them forced over
     // fixed-stride batches
     if (mode == MODE_VERIFY) {
-        if (variant == 41 || variant == 18 || variant == 62) variant = 63;  // emit forms of 63
+        if (variant == 41 || variant == 18 || variant == 62 || variant == 94) variant = 63;  // emit forms of 63
         if (variant == 20 || variant % 64 == 61) variant = 60;              // emit forms of 60
     }
 #ifdef SMOL_EXP
     const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63 ||
-                        variant == 18 || variant == 20 || variant == 41;
+                        variant == 18 || variant == 20 || variant == 41 || variant == 94;
     const bool dw_ok = (mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc;
 #else
-    const bool dw_var = variant == 60 || variant == 63 || variant == 41;
+    const bool dw_var = variant == 60 || variant == 63 || variant == 41 || variant == 94;
     const bool dw_ok = (mode == MODE_VERIFY || (mode == MODE_EMIT && variant != 60)) && has_desc && !nhc;
 #endif
     if (dw_var) {
@@ -381,7 +373,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         return SMOL_OK;
     }
     const Pick k = pick_kernel(ctx, mode, b, p);
-    if (k.family == F_XWALK && mode == MODE_EMIT && staged_variant(k.variant)) {
+    if (mode == MODE_EMIT && ((k.family == F_XWALK && staged_variant(k.variant)) ||
+                              (k.family == F_DWALK && staged_desc_variant(k.variant)))) {
         // staged emit: the field entries of kStageChunk records at a time (scratch owned by the context),
         // each chunk's staging launch followed by its segment pass
         const uint64_t want = b->n < kStageChunk ? b->n : kStageChunk;
@@ -399,10 +392,11 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         for (uint64_t i0 = 0; i0 < b->n; i0 += kStageChunk) {
             KParams q = p;
             q.n = b->n - i0 < kStageChunk ? b->n - i0 : kStageChunk;
-            q.buf = d_buf + i0 * b->stride;
+            if (b->desc) q.desc = b->desc + i0;
+            else q.buf = d_buf + i0 * b->stride;
             if (d_status) q.status = d_status + i0;
             q.stage = ctx->stage;
-            const hipError_t e = launch_xwalk(mode, k.variant, q, s);
+            const hipError_t e = k.family == F_DWALK ? launch_dwalk(mode, k.variant, q, s) : launch_xwalk(mode, k.variant, q, s);
             if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         }
         return SMOL_OK;

@@ -51,7 +51,12 @@ constexpr int U = 4;        // load instructions in flight per wavefront
 // policy instead of non-temporal (62 = both, 63 = bit 1 alone); bit 2: the 2-B fields stored
 // non-temporal (experiments: 18 = 63 + bit 2, 20 = 60's emit + bit 2); bit 3: the window's 16
 // chunks summed from LDS, the stream starting at chunk 16 (41 = 63 + bit 3: the product's
-// descriptor-batch emit since late round 5).
+// descriptor-batch emit since late round 5); bit 4: staged (variant 94 = 61 + bits 1, 3 and 4, round 6):
+// a record whose fields the whole segments cover (bit 0's rule, all or nothing) writes nothing here and
+// stages one 8-B entry (its two field offsets and values) in p.stage for the segment pass
+// (seg_pass_desc_kernel); any other record stores its fields here as 2-B writes and stages ~0.
+// tools/probe_wtax.hip: field writes that land while a read stream runs cost 65-90 ps each, the same
+// segments loaded again and written in a pass of their own ~40 ps.
 template <int MODE, bool NOSTORE, bool GROUPS = false, int SEGF = 0>
 __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     using namespace dwalk;
@@ -96,6 +101,7 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
 
     // ---- the windows: instruction w, lane l: record 4 w + l / 16, chunk l % 16 ----
     constexpr bool SEG = (SEGF & 1) != 0 && MODE == MODE_EMIT;
+    constexpr bool STAGE = (SEGF & 16) != 0 && SEG;
     constexpr bool WNT = (SEGF & 2) == 0;
     const bool mine = (uint32_t)gw < cnt;
     const uint64_t r = rw0 + (uint64_t)gw;
@@ -158,6 +164,15 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
             auto whole = [&](int32_t rel) { return rB <= rA + 64 && rel + 64 <= wend && (rel >= 0 || prev_ok); };
             if (whole(rA)) wsA = a0 + (int64_t)rA;
             if (rB != rA && whole(rB)) wsB = a0 + (int64_t)rB;
+        }
+        if constexpr (STAGE) {  // all or nothing: staged when the segments cover every field byte
+            auto cov = [&](uint32_t fo) {
+                const uint64_t x0 = (a0 + fo) & ~63ull, x1 = (a0 + fo + 1) & ~63ull;
+                return (x0 == wsA || x0 == wsB) && (x1 == wsA || x1 == wsB);
+            };
+            const bool staged = wsA != ~0ull && f[2] == NO_FIELD && (f[0] == NO_FIELD || cov(f[0])) &&
+                                (f[1] == NO_FIELD || cov(f[1]));
+            if (!staged) wsA = wsB = ~0ull;
         }
     }
     wave_lds_sync();
@@ -277,10 +292,67 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
             if constexpr (NOSTORE) asm volatile("" ::"v"(x), "v"(dst));
             else *(GMEM u32x2*)dst = x;
         };
-        if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
-        if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
+        if constexpr (STAGE) {
+            if (mine && lane == 0) {
+                uint64_t e = ~0ull;
+                if (wsA != ~0ull) {
+                    uint32_t f[3];
+                    emit_fields(g, f);
+                    auto fv = [&](uint32_t fo) -> uint64_t {
+                        return fo == NO_FIELD ? 0xffffull : (uint64_t)fo | ((uint64_t)((winb[hd + fo] << 8) | winb[hd + fo + 1]) << 32);
+                    };
+                    const uint64_t e0 = fv(f[0]), e1 = fv(f[1]);
+                    e = (e0 & 0xffffull) | ((e1 & 0xffffull) << 16) | (e0 >> 32 << 32) | (e1 >> 32 << 48);
+                }
+                __builtin_nontemporal_store(e, (GMEM uint64_t*)(p.stage + r));
+            }
+        } else {
+            if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
+            if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
+        }
     } else {
         if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE, (SEGF & 4) != 0>(p, g, a1, rd, winb, hd, a0, r, lane);
+    }
+}
+
+// The segment pass of the staged descriptor-batch emit (variant 94): 8 lanes per record; a record
+// with an entry loads the 64-B segment(s) holding its fields (default cache policy), patches the
+// field bytes in and stores each segment whole, write-through and non-temporal (sc0 sc1 nt; a plain
+// or nt store after the default-policy load stays dirty on chip and is written back inside the next
+// read stream: tools/probe_wtax.hip, 0.054 against 0.106 ms per C2 pass).  Records anywhere in the
+// buffer: 64-bit addresses, so the store is written as the instruction (global_store_dwordx2 with its
+// cache-policy bits; a vector store).  The segments are the staging launch's decision (the whole-
+// segment rule of variant 61), so no two groups write one segment and no other write touches them.
+__device__ __forceinline__ uint64_t patch_field(uint64_t x, int64_t k, uint32_t v) {
+    if (k >= 0 && k < 8) x = (x & ~(0xffull << (8 * k))) | ((uint64_t)((v >> 8) & 0xffu) << (8 * k));
+    if (k + 1 >= 0 && k + 1 < 8) x = (x & ~(0xffull << (8 * (k + 1)))) | ((uint64_t)(v & 0xffu) << (8 * (k + 1)));
+    return x;
+}
+
+__global__ __launch_bounds__(256) void seg_pass_desc_kernel(KParams p) {
+    const uint64_t r = (uint64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+    const int l = (int)(threadIdx.x & 7);
+    if (r >= p.n) return;
+    const uint64_t e = __builtin_nontemporal_load((const GMEM uint64_t*)(p.stage + r));
+    if (e == ~0ull) return;
+    const uint64_t off = p.desc ? *(const GMEM uint64_t*)((uint64_t)p.desc + 16 * r) : r * p.stride;
+    const uint32_t f0 = (uint32_t)(e & 0xffffu), f1 = (uint32_t)((e >> 16) & 0xffffu);
+    const uint32_t v0 = (uint32_t)((e >> 32) & 0xffffu), v1 = (uint32_t)(e >> 48);
+    const uint64_t a0 = (uint64_t)p.buf + off;
+    const uint32_t lo = min(f0 == 0xffffu ? 0xffffu : f0, f1 == 0xffffu ? 0xffffu : f1);
+    const uint32_t hi = max(f0 == 0xffffu ? 0u : f0 + 2, f1 == 0xffffu ? 0u : f1 + 2);
+    const uint64_t sA = (a0 + lo) & ~63ull, sB = (a0 + hi - 1) & ~63ull;
+    const uint64_t wA = sA + 8u * (uint32_t)l, wB = sB + 8u * (uint32_t)l;
+    // both loads before either store (stores count in vmcnt with the loads, in order)
+    uint64_t xa = *(const GMEM uint64_t*)wA;
+    uint64_t xb = sB != sA ? *(const GMEM uint64_t*)wB : 0ull;
+    if (f0 != 0xffffu) xa = patch_field(xa, (int64_t)(a0 + f0) - (int64_t)wA, v0);
+    if (f1 != 0xffffu) xa = patch_field(xa, (int64_t)(a0 + f1) - (int64_t)wA, v1);
+    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(wA), "v"(xa) : "memory");
+    if (sB != sA) {
+        if (f0 != 0xffffu) xb = patch_field(xb, (int64_t)(a0 + f0) - (int64_t)wB, v0);
+        if (f1 != 0xffffu) xb = patch_field(xb, (int64_t)(a0 + f1) - (int64_t)wB, v1);
+        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(wB), "v"(xb) : "memory");
     }
 }
 
@@ -288,9 +360,19 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
 #ifndef SMOL_EXP
     // the product's forms: 63 (verify / emit), 41 (emit), 60 (verify)
     if (!(variant == 63 && (mode == MODE_VERIFY || mode == MODE_EMIT)) && !(variant == 60 && mode == MODE_VERIFY) &&
-        !(variant == 41 && mode == MODE_EMIT))
+        !(variant == 41 && mode == MODE_EMIT) && !(variant == 94 && mode == MODE_EMIT))
         return hipErrorInvalidValue;
 #endif
+    if (variant == 94 && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
+        if (!p.stage || p.n > kStageChunk) return hipErrorInvalidValue;
+        note_launch(KERN_DWALK, 94u, dwalk::G, dwalk::U);
+        const uint32_t b = grid_blocks((p.n + dwalk::GPB - 1) / dwalk::GPB, kMaxGridBlocks);
+        hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27>), dim3(b), dim3(256), 0, s, p);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(seg_pass_desc_kernel, dim3((uint32_t)((p.n + 31) / 32)), dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     const uint64_t per = (uint64_t)dwalk::GPB;
     note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
     const uint64_t span = kMaxGridBlocks * per;

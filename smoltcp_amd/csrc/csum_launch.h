@@ -135,6 +135,7 @@ hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s);
 // the segment pass writes the field segments whole (csum_xwalk.hip).  Records per launch pair:
 constexpr uint64_t kStageChunk = 1ull << 21;
 inline bool staged_variant(int v) { return v == 80 || v == 81; }
+inline bool staged_desc_variant(int v) { return v == 94; }  // csum_dwalk.hip
 
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
 struct SynthParams {

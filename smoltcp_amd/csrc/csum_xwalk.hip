@@ -146,15 +146,25 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
             for (int s = 0; s < (HALF ? 1 : NS); ++s) {
                 const uint32_t k = (uint32_t)(64 * s + wl);
                 const uint32_t o = k < nload[j] ? 16u * k : 0x80000000u;
-                if ((NTS == 32 || HINT) && s == 0) {  // some header lanes with the default cache policy
+                if ((NTS == 32 || (HINT >= 1 && HINT <= 7)) && s == 0) {  // some header lanes with the default cache policy
                     // HINT 1 (and NTS 32): the segments of record offsets [10, 28) (an IPv4 record's fields);
-                    // 2: those of [0, 64); 3: the whole 256-B window; 4: the segment of offset 10 only
+                    // 2: those of [0, 64); 3: the whole 256-B window; 4: the segment of offset 10 only;
+                    // 5: the 16-B chunk of offset 10 only; 6: the segment of the record's first byte;
+                    // 7: the line's first segment (lanes 0-3)
                     const uint32_t sg = (uint32_t)wl >> 2, h = head[j];
                     const bool c = (HINT == 0 || HINT == 1) ? (sg == (h + 10u) >> 6 || sg == (h + 27u) >> 6)
                                    : HINT == 2 ? (sg == h >> 6 || sg == (h + 63u) >> 6)
                                    : HINT == 3 ? wl < 16
-                                               : sg == (h + 10u) >> 6;
+                                   : HINT == 4 ? sg == (h + 10u) >> 6
+                                   : HINT == 5 ? (uint32_t)wl == (h + 10u) >> 4
+                                   : HINT == 6 ? sg == h >> 6
+                                               : wl < 4;
                     if (c) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
+                    else v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 2);
+                } else if ((HINT == 8 && s == 0) || (HINT == 9 && s == 1) || HINT == 10) {
+                    // 8: instruction 0 split in two (lanes 0-3 / the rest), both non-temporal; 9: lanes 0-3 of
+                    // instruction 1 with the default policy; 10: lanes 0-3 of every instruction
+                    if (wl < 4) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, HINT == 8 ? 2 : 0);
                     else v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 2);
                 } else if (((NTS == 4 || NTS == 5) && s == 0) || NTS == 8) v[s][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
                 else if (NTS == 16 && s == 0) {  // the header lines cached, the rest of the KiB nt
@@ -428,12 +438,30 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
-    if (variant >= 84 && variant <= 86) {  // verify hint forms (emit: 47's, as 82): 84 [0, 64), 85 the window, 86 offset 10
+    if (variant >= 90 && variant <= 92) {  // verify hint forms 8-10 (emit: 57)
         if (mode == MODE_VERIFY) {
-            if (variant == 84) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 2>), dim3(blocks), dim3(256), 0, s, p);
-            else if (variant == 85) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 3>), dim3(blocks), dim3(256), 0, s, p);
-            else hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 4>), dim3(blocks), dim3(256), 0, s, p);
-        } else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+            if (variant == 90) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 8>), dim3(blocks), dim3(256), 0, s, p);
+            else if (variant == 91) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 9>), dim3(blocks), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 10>), dim3(blocks), dim3(256), 0, s, p);
+        } else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if (variant >= 84 && variant <= 88) {  // verify hint forms 2-6 (emit: 57 with the same hint)
+        if (mode == MODE_VERIFY) {
+            switch (variant) {
+                case 84: hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 2>), dim3(blocks), dim3(256), 0, s, p); break;
+                case 85: hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 3>), dim3(blocks), dim3(256), 0, s, p); break;
+                case 86: hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 4>), dim3(blocks), dim3(256), 0, s, p); break;
+                case 87: hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 5>), dim3(blocks), dim3(256), 0, s, p); break;
+                default: hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 6>), dim3(blocks), dim3(256), 0, s, p); break;
+            }
+        } else {
+            switch (variant) {
+                case 86: hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 4>), dim3(blocks), dim3(256), 0, s, p); break;
+                case 87: hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 5>), dim3(blocks), dim3(256), 0, s, p); break;
+                default: hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 1>), dim3(blocks), dim3(256), 0, s, p); break;
+            }
+        }
         return;
     }
     if constexpr (R == 8) {
@@ -481,9 +509,14 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #endif
-    const bool seg = variant % 64 == 47 || variant == 57;
+    const bool seg = variant % 64 == 47 || variant == 57 || variant == 89;
     if (mode == MODE_VERIFY) {  // (57: 47's verify)
-        hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
+        // 89 (round 6): lanes 0-3 of each record's first instruction (the first 64 B of its first line)
+        // load with the default cache policy, the rest non-temporal: C2 verify 0.2342 -> 0.2259 ms
+        // (bench lines interleaved on one box, profiles/r06_experiments/verify_hint_ab.txt); the split
+        // itself without the policy change (90) gains nothing
+        if (variant == 89) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
 #ifdef SMOL_EXP
@@ -493,7 +526,7 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #endif
-    if (variant == 57) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+    if (variant == 57 || variant == 89) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
     else if (seg) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true>), dim3(blocks), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
 }

@@ -4,6 +4,7 @@ scalar host mirrors are bit-exact against the oracle, and the batched entry poin
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -144,8 +145,25 @@ def test_variant_lists():
 
     L = _lib.lib()
     built = [v for v in range(-1, 128) if L.smol_csum_tool_variant_built(v)]
-    assert built == [-1, 5, 7, 13, 17, 21, 39, 41, 44, 47, 57, 60, 63], built
+    assert built == [-1, 5, 7, 13, 17, 21, 39, 41, 44, 47, 57, 60, 63, 89, 94], built
     if os.path.exists(_lib.EXP_LIB_PATH):
         X = _lib.lib(_lib.EXP_LIB_PATH)
         exp = {v for v in range(-1, 128) if X.smol_csum_tool_variant_built(v)}
         assert set(built) < exp and {0, 1, 3, 4, 16, 19, 23, 28, 29, 31, 37, 38, 42, 56, 80, 81, 82, 83, 64 + 37, 64 + 44, 64 + 47} <= exp
+
+
+def test_dispatch_table_matches_sweeps():
+    """smoltcp_amd/csrc/dispatch_table.inc (the fixed-stride dispatch, csum_api.cpp xwalk_auto) is what
+    tools/gen_dispatch_table.py makes from the committed length sweeps (profiles/r06_dispatch_sweep_*),
+    and C2's 1500-B records take the transposed walk with the first-load hint (verify) and with
+    non-temporal segments (emit)."""
+    import subprocess
+
+    from tests.dispatch_table import fixed_launch
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_dispatch_table.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert fixed_launch("verify", 1500, 1500) == ("xwalk_kernel", 89)
+    assert fixed_launch("emit", 1500, 1500) == ("xwalk_kernel", 57)
+    assert fixed_launch("verify", 1000, 1000) == ("csum_kernel", 5)

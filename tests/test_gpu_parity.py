@@ -282,7 +282,7 @@ def _mixed_records(rng, n=240):
     return recs
 
 
-@pytest.mark.parametrize("variant", [56, 60, 61, 62, 63, 18, 20, 41])
+@pytest.mark.parametrize("variant", [56, 60, 61, 62, 63, 18, 20, 41, 94])
 def test_dwalk_descriptor_batches(eng, variant):
     """The descriptor walks (63: the product's descriptor verify / emit, cached header windows; 60:
     non-temporal windows; experiments build: 56, and 61 / 62 = 60's / 63's emit with whole field
@@ -851,6 +851,58 @@ def test_staged_emit_chunks(eng, variant):
         assert np.array_equal(got[lo * L: hi * L].cpu().numpy(), want), lo
 
 
+def test_staged_descriptor_emit_chunks(eng):
+    """The staged descriptor-batch emit (variant 94: field entries, then the segment pass) over more
+    descriptors than one staging chunk (2^21), short packed records at odd offsets and shuffled ones,
+    writes the same bytes as the in-place descriptor emit (variant 41, oracle-checked above), and the
+    oracle agrees on records at the chunk seams."""
+    eng.need(94)
+    rng = np.random.default_rng(94)
+    n = (1 << 21) + 4099
+    lens = rng.integers(64, 200, n).astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    total = int(offs[-1] + lens[-1]) + 16
+    for order in (None, rng.permutation(n)):
+        o, l = (offs, lens) if order is None else (offs[order], lens[order])
+        batch = E.Batch.from_records(o, l, E.KIND_IP, "cuda:0")
+        base = torch.zeros(total + 1, dtype=torch.uint8, device="cuda:0")
+        view = base[1:]
+        eng.synth(view, batch, E.SYNTH_TCP4, seed=9)
+        ref = base.clone()
+        eng.set_variant(41)
+        try:
+            eng.emit(ref[1:], batch)
+        finally:
+            eng.set_variant(-1)
+        eng.set_variant(94)
+        try:
+            eng.emit(view, batch)
+            assert (eng.last_launch()["kernel"], eng.last_launch()["variant"]) == ("dwalk_kernel", 94)
+        finally:
+            eng.set_variant(-1)
+        torch.cuda.synchronize()
+        assert torch.equal(base, ref)
+    host = synth_host = None
+    base = torch.zeros(total + 1, dtype=torch.uint8, device="cuda:0")
+    batch = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0")
+    eng.synth(base[1:], batch, E.SYNTH_TCP4, seed=10)
+    synth_host = base[1:].cpu().numpy().copy()
+    eng.set_variant(94)
+    try:
+        eng.emit(base[1:], batch)
+    finally:
+        eng.set_variant(-1)
+    host = base[1:].cpu().numpy()
+    for lo in (0, (1 << 21) - 50, n - 60):
+        hi = min(n, lo + 100)
+        a, b = int(offs[lo]), int(offs[hi - 1] + lens[hi - 1])
+        want = synth_host[a:b].copy()
+        d = P.oracle_desc(offs[lo:hi] - np.uint64(a), lens[lo:hi], E.KIND_IP)
+        oracle.batch_emit(want, d, hi - lo, 0, 0, E.KIND_IP, CAPS_DEFAULT)
+        assert np.array_equal(host[a:b], want), lo
+
+
 def _wide_case(eng, variant, kname, host, off, n, L, kind, caps, stride=None):
     stride = stride or L
     batch = E.Batch.fixed(n, stride, L, kind)
@@ -1083,3 +1135,43 @@ def test_launch_records_copy_and_nhc(eng):
         assert np.array_equal(got, ref), per
         assert np.array_equal(nst, ref_nv), per
         assert np.array_equal(gotn, ref_n), per
+
+
+def test_dispatch_table_every_row(eng):
+    """Every row of the measured fixed-stride dispatch table (csum_api.cpp xwalk_auto,
+    dispatch_table.inc, round 6): at each row's first and last length, a length that is not a multiple of
+    64 and a gapped stride, emit then verify (1/5 of the records corrupted) with the library's own
+    choice, no variant forced, against the oracle; the kernel the table names (kernel_for) is the one
+    that ran.  Also the lengths just outside the table (1023, 9024)."""
+    rng = np.random.default_rng(64)
+    cases = []
+    for k in range(125):
+        a = 1024 + 64 * k
+        cases += [(a, a), (a + 63, a + 63), (a + 28, a + 28), (a + 28, a + 92)]
+    cases += [(1023, 1023), (9024, 9024), (9024, 9100)]
+    for i, (L, stride) in enumerate(cases):
+        n = 19  # two full wavefronts of 8 records and a partial one
+        profile = (E.SYNTH_UDP4, E.SYNTH_TCP4, E.SYNTH_V6MIX)[i % 3]
+        recs = torch.zeros(n * L + 64, dtype=torch.uint8, device="cuda:0")
+        pb = E.Batch.fixed(n, L, L, E.KIND_IP)
+        eng.synth(recs, pb, profile, seed=L + i)
+        r = recs.cpu().numpy()[: n * L].reshape(n, L)
+        host = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+        for j in range(n):
+            host[j * stride: j * stride + L] = r[j]
+        batch = E.Batch.fixed(n, stride, L, E.KIND_IP)
+        d = torch.from_numpy(host.copy()).cuda()
+        want_e = eng.kernel_for("emit", batch)
+        eng.emit(d, batch)
+        assert eng.last_launch()["kernel"] == want_e, (L, stride)
+        ref = host.copy()
+        oracle.batch_emit(ref, None, n, stride, L, E.KIND_IP, CAPS_DEFAULT)
+        got = d.cpu().numpy()
+        assert np.array_equal(got, ref), (L, stride, want_e, np.nonzero(got != ref)[0][:8])
+        for j in range(0, n, 5):
+            ref[j * stride + int(rng.integers(0, L))] ^= 0x21
+        d = torch.from_numpy(ref.copy()).cuda()
+        want_v = eng.kernel_for("verify", batch)
+        st = eng.verify(d, batch).cpu().numpy()
+        assert eng.last_launch()["kernel"] == want_v, (L, stride)
+        assert np.array_equal(st, oracle.batch_verify(ref, None, n, stride, L, E.KIND_IP, CAPS_DEFAULT)), (L, stride, want_v)

@@ -26,6 +26,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from smoltcp_amd import engine as E  # noqa: E402
+from tests.dispatch_table import fixed_launch
 from tests.engines import VariantEngine  # noqa: E402
 
 SEG_VARIANTS = (23, 24, 25, 26, 27, 28)
@@ -296,4 +297,7 @@ def test_field_stores_flag(eng):
         torch.cuda.synchronize()
         assert bool((payload == K).all()), L
         ll = eng.last_launch()
-        assert (ll["kernel"], ll["variant"]) == (("csum_kernel", 5) if L == 1600 else ("xwalk_kernel", 44)), (L, ll)
+        # SMOL_BATCH_FIELD_STORES: the table's kernel with 2-B field stores (the walk kernel's 5, the
+        # transposed walk's 44)
+        kern, _ = fixed_launch("emit", L, L)
+        assert (ll["kernel"], ll["variant"]) == ((kern, 44) if kern == "xwalk_kernel" else (kern, 5)), (L, ll)

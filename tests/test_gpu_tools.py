@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from smoltcp_amd import engine as E
+from tests.dispatch_table import fixed_launch
 from tests.engines import VariantEngine
 
 pytestmark = pytest.mark.gpu
@@ -71,25 +72,21 @@ def test_last_launch_families(eng):
     ll = eng.last_launch()
     # packed fixed-stride emit of 1400-1580-B records (not multiples of 64 B): the transposed walk
     # with its field segments stored non-temporal
-    assert (ll["kernel"], ll["variant"], ll["G"]) == ("xwalk_kernel", 57, 8), ll
+    assert (ll["kernel"], ll["variant"]) == fixed_launch("emit", L, L), ll
     eng.verify(buf, b)
     ll = eng.last_launch()
-    # packed fixed-stride verify of 1473 .. 8065-B records: the transposed walk, 8 records per wavefront
-    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("xwalk_kernel", 47, 8, 2), ll
-    X, W = "xwalk_kernel", "csum_kernel"
-    for LL, stride, op, want in ((1320, 1320, "verify", (W, 5, 8)), (1500, 1501, "verify", (W, 5, 8)),
-                                 (2500, 2500, "emit", (X, 47, 16)), (2500, 2500, "verify", (X, 47, 16)),
-                                 (1500, 1500, "emit", (X, 57, 8)), (1600, 1600, "emit", (W, 39, 8)),
-                                 (1320, 1320, "emit", (W, 39, 8)), (1500, 1564, "emit", (W, 39, 8)), (9000, 9000, "verify", (W, 5, None)),
-                                 (8000, 8000, "emit", (X, 47, 32)), (1536, 1536, "verify", (W, 5, 8)), (12000, 12000, "emit", (W, 39, None)),
-                                 (12000, 12000, "verify", (W, 5, None)), (2500, 2564, "emit", (X, 47, 16)),
-                                 (1500, 1564, "verify", (W, 5, 8)), (1700, 1764, "verify", (X, 47, 8))):
-        bb = E.Batch.fixed(8, stride, LL, E.KIND_IP)
-        t = torch.zeros(8 * stride + 64, dtype=torch.uint8, device="cuda:0")
-        getattr(eng, op)(t, bb)
-        ll = eng.last_launch()
-        assert (ll["kernel"], ll["variant"]) == want[:2], (LL, stride, op, ll)
-        assert want[2] is None or ll["G"] == want[2], (LL, stride, op, ll)
+    # the dispatch table's choices (tests/dispatch_table.py reads smoltcp_amd/csrc/dispatch_table.inc)
+    assert (ll["kernel"], ll["variant"]) == fixed_launch("verify", L, L), ll
+    for LL, stride in ((1320, 1320), (1500, 1501), (2500, 2500), (1600, 1600), (1500, 1564), (9000, 9000),
+                       (8000, 8000), (1536, 1536), (12000, 12000), (2500, 2564), (1700, 1764), (1024, 1024)):
+        for op in ("emit", "verify"):
+            bb = E.Batch.fixed(8, stride, LL, E.KIND_IP)
+            t = torch.zeros(8 * stride + 64, dtype=torch.uint8, device="cuda:0")
+            getattr(eng, op)(t, bb)
+            ll = eng.last_launch()
+            assert (ll["kernel"], ll["variant"]) == fixed_launch(op, LL, stride), (LL, stride, op, ll)
+            if ll["kernel"] == "xwalk_kernel":  # 8 / 4 / 2 / 1 records per wavefront by length
+                assert ll["G"] == 64 // (8 if LL <= 1921 else 4 if LL <= 3969 else 2 if LL <= 8065 else 1), (LL, ll)
     offs = np.arange(n, dtype=np.uint64) * L
     bd = E.Batch.from_records(offs, np.full(n, L, np.uint32), E.KIND_IP, "cuda:0")
     # descriptor batches: the per-group descriptor walk (csum_dwalk.hip, cached header windows),
