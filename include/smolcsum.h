@@ -206,14 +206,19 @@ int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
  * filled).  An ICMPv4 DstUnreachable / TimeExceeded message's embedded IPv4 header gets its header
  * checksum first, under caps.ipv4, as Icmpv4Repr::emit writes it with Ipv4Repr::emit
  * (src/wire/icmpv4.rs:520-543).  `d_status` (nullable) receives SMOL_ST_MALFORMED /
- * SMOL_ST_UNSUPPORTED per record.  One kernel on `stream`; records must not overlap.  The kernel
- * writes the 64-byte segment around a record's fields whole where that is race-free within the
+ * SMOL_ST_UNSUPPORTED per record.  Kernels on `stream` only; records must not overlap.  The kernels
+ * write the 64-byte segment around a record's fields whole where that is race-free within the
  * call: the segment's other bytes, which may belong to the records just before and after it in
  * the batch (contiguous with it in memory, no field of theirs in the segment), are written back
- * with the values the kernel read.  Bytes outside the batch's records are never written.  So
+ * with the values the kernels read.  Bytes outside the batch's records are never written.  So
  * nothing else may write the batch's records while the call runs, the same rule copy-emit states,
- * unless the batch sets SMOL_BATCH_FIELD_STORES (fields only).  No device memory is allocated: the
- * calls may be captured in a HIP graph. */
+ * unless the batch sets SMOL_BATCH_FIELD_STORES (fields only).  Descriptor batches of records that
+ * lie back to back take the staged form (one launch stages each record's field values in the
+ * context's scratch, a second one writes the field segments, per 2^21 records): the context owns
+ * ~17 MB of device scratch, allocated by smol_csum_ctx_create, and orders a staged emit issued on
+ * another stream after the previous one (an event wait), so emits on one context may use several
+ * streams.  No device memory is allocated by a batched call: the calls may be captured in a HIP
+ * graph. */
 int smol_csum_batch_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                          const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
 

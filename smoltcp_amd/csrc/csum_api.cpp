@@ -27,8 +27,14 @@ struct smol_csum_ctx {
     int xcd_remap;        // walk kernel: each XCD's blocks take a contiguous range of records
                           // (-1: automatic, xcd_remap_auto; 0 / 1: forced, tooling)
     uint64_t launch_records;  // records per kernel launch (0: the whole batch in one launch)
-    uint64_t* stage;          // staged emit's field entries (variants 80 / 81), grown on first use
-    uint64_t stage_cap;       // entries `stage` holds
+    // staged emit (variant 94; 80 / 81 experiments): the field entries and per-8-record flags of one
+    // chunk of kStageChunk records, allocated with the context (no allocation in a batched call);
+    // stage_stream / stage_done order a staged emit on another stream after the previous one
+    uint64_t* stage;
+    uint32_t* stage_flags;
+    void* stage_stream;
+    bool stage_recorded;
+    hipEvent_t stage_done;
 };
 
 namespace smolcsum {
@@ -170,7 +176,7 @@ int field_store_variant(int variant, bool has_desc) {
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62 || variant == 18) return 63;  // (63 stores 2-B fields only)
     if (variant == 20) return 60;
-    if (variant == 41 || variant == 94) return 41;
+    if (variant == 41 || variant == 94 || variant == 95) return 41;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
@@ -186,7 +192,7 @@ bool variant_built(int v) {
         default: break;
     }
 #ifdef SMOL_EXP
-    if ((v >= 80 && v <= 88) || v == 90 || v == 91 || v == 92) return true;
+    if ((v >= 80 && v <= 88) || v == 90 || v == 91 || v == 92 || v == 95) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -289,12 +295,12 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     // 18 / 20 (non-temporal 2-B fields) in the experiments build, which also runs them forced over
     // fixed-stride batches
     if (mode == MODE_VERIFY) {
-        if (variant == 41 || variant == 18 || variant == 62 || variant == 94) variant = 63;  // emit forms of 63
+        if (variant == 41 || variant == 18 || variant == 62 || variant == 94 || variant == 95) variant = 63;  // emit forms of 63
         if (variant == 20 || variant % 64 == 61) variant = 60;              // emit forms of 60
     }
 #ifdef SMOL_EXP
     const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63 ||
-                        variant == 18 || variant == 20 || variant == 41 || variant == 94;
+                        variant == 18 || variant == 20 || variant == 41 || variant == 94 || variant == 95;
     const bool dw_ok = (mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc;
 #else
     const bool dw_var = variant == 60 || variant == 63 || variant == 41 || variant == 94;
@@ -375,19 +381,12 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
     const Pick k = pick_kernel(ctx, mode, b, p);
     if (mode == MODE_EMIT && ((k.family == F_XWALK && staged_variant(k.variant)) ||
                               (k.family == F_DWALK && staged_desc_variant(k.variant)))) {
-        // staged emit: the field entries of kStageChunk records at a time (scratch owned by the context),
-        // each chunk's staging launch followed by its segment pass
-        const uint64_t want = b->n < kStageChunk ? b->n : kStageChunk;
-        if (ctx->stage_cap < want) {
-            if (ctx->stage) (void)hipFree(ctx->stage);
-            ctx->stage = nullptr;
-            ctx->stage_cap = 0;
-            hipError_t ea = hipMalloc(&ctx->stage, want * sizeof(uint64_t));
-            if (ea != hipSuccess) {
-                ctx->stage = nullptr;
-                return hip_fail(ea, "hipMalloc (staged emit entries)");
-            }
-            ctx->stage_cap = want;
+        // staged emit: kStageChunk records at a time through the context's entries, each chunk's staging
+        // launch followed by its segment pass.  A call on another stream than the previous staged emit
+        // first waits for that one (the entries are the context's).
+        if (ctx->stage_recorded && ctx->stage_stream != stream) {
+            hipError_t ew = hipStreamWaitEvent(s, ctx->stage_done, 0);
+            if (ew != hipSuccess) return hip_fail(ew, "hipStreamWaitEvent (staged emit)");
         }
         for (uint64_t i0 = 0; i0 < b->n; i0 += kStageChunk) {
             KParams q = p;
@@ -396,9 +395,14 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
             else q.buf = d_buf + i0 * b->stride;
             if (d_status) q.status = d_status + i0;
             q.stage = ctx->stage;
+            q.stage_flags = ctx->stage_flags;
             const hipError_t e = k.family == F_DWALK ? launch_dwalk(mode, k.variant, q, s) : launch_xwalk(mode, k.variant, q, s);
             if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         }
+        hipError_t er = hipEventRecord(ctx->stage_done, s);
+        if (er != hipSuccess) return hip_fail(er, "hipEventRecord (staged emit)");
+        ctx->stage_stream = stream;
+        ctx->stage_recorded = true;
         return SMOL_OK;
     }
     hipError_t e = hipSuccess;
@@ -446,18 +450,36 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
         (void)hipFree(dummy);
         return hip_fail(e, "hipMemset");
     }
+    uint64_t* stage = nullptr;
+    uint32_t* flags = nullptr;
+    hipEvent_t done = nullptr;
+    e = hipMalloc(&stage, kStageChunk * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc(&flags, (kStageChunk / 8 + 64) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        (void)hipFree(dummy);
+        if (stage) (void)hipFree(stage);
+        if (flags) (void)hipFree(flags);
+        return hip_fail(e, "context allocation");
+    }
     auto* c = new (std::nothrow) smol_csum_ctx;
     if (!c) {
         (void)hipFree(dummy);
+        (void)hipFree(stage);
+        (void)hipFree(flags);
+        (void)hipEventDestroy(done);
         return SMOL_ENOMEM;
     }
     c->dummy = dummy;
+    c->stage = stage;
+    c->stage_flags = flags;
+    c->stage_stream = nullptr;
+    c->stage_recorded = false;
+    c->stage_done = done;
     c->tile_records = 32;
     c->max_blocks_set = false;
     c->xcd_remap = -1;
     c->launch_records = 0;
-    c->stage = nullptr;
-    c->stage_cap = 0;
     c->device = device;
     c->num_cu = cus;
     c->max_blocks = kNaturalGrid;
@@ -472,7 +494,9 @@ int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
     {
         DeviceGuard guard(ctx->device);
         (void)hipFree(ctx->dummy);
-        if (ctx->stage) (void)hipFree(ctx->stage);
+        (void)hipFree(ctx->stage);
+        (void)hipFree(ctx->stage_flags);
+        (void)hipEventDestroy(ctx->stage_done);
     }
     delete ctx;
     return SMOL_OK;

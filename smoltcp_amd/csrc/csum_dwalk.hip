@@ -40,6 +40,7 @@ constexpr int WAVES = 4;
 constexpr int GPB = WAVES * R;
 constexpr int WIN_CH = 16;  // the LDS window: 256 B from the record's 128-B line
 constexpr int U = 4;        // load instructions in flight per wavefront
+constexpr uint32_t kStageMinBytes = 1024;  // STAGE: the wavefront's mean record length to stage at
 
 }  // namespace dwalk
 
@@ -58,7 +59,7 @@ constexpr int U = 4;        // load instructions in flight per wavefront
 // tools/probe_wtax.hip: field writes that land while a read stream runs cost 65-90 ps each, the same
 // segments loaded again and written in a pass of their own ~40 ps.
 template <int MODE, bool NOSTORE, bool GROUPS = false, int SEGF = 0>
-__global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 32) ? 8 : 1))) void dwalk_kernel(KParams p) {
     using namespace dwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
     __shared__ u32x4 win[GPB][WIN_CH];
@@ -146,7 +147,15 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     // fields end 64 bytes or more before its end keeps its segments inside itself; the window must
     // hold the whole segment.  The rest are stored as 2-B fields.
     uint64_t wsA = ~0ull, wsB = ~0ull;
+    // STAGE: a wavefront stages its records only when they lie back to back and average at least
+    // kStageMinBytes each (wave-uniform); otherwise it runs variant 41's finish, 2-B field stores.
+    // Measured in bench.py's step order (tools/exp_r06_desc_step.py, profiles/r06_experiments/
+    // desc_layouts_step_41_94.jsonl), staging every record: C3 packed step 1.598 -> 1.503 ms and
+    // 500-3000-B records 0.703 -> 0.685, but 64-1500-B records 0.389 -> 0.467 and gapped / shuffled C3
+    // +1 / +1.6 % (not back to back: few segments may go out whole)
+    const bool stage_wave = STAGE && contig && A[cnt - 1] + L[cnt - 1] - A[0] >= (uint64_t)cnt * dwalk::kStageMinBytes;
     if constexpr (SEG) {
+      if (!STAGE || stage_wave) {
         uint32_t f[3], flo = NO_FIELD, fhi = 0;
         emit_fields(g, f);
         for (int j = 0; j < 3; ++j)
@@ -174,6 +183,7 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
                                 (f[1] == NO_FIELD || cov(f[1]));
             if (!staged) wsA = wsB = ~0ull;
         }
+      }
     }
     wave_lds_sync();
     uint32_t S1[R];
@@ -280,7 +290,10 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
         }
     }
     // ---- finish: the walk kernel's gates ----
-    if constexpr (SEG) {
+    if (STAGE && !stage_wave) {  // (wave-uniform) variant 41's finish, nothing staged
+        if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane);
+        if (wl == 0) p.stage_flags[rw0 / R] = 0u;  // the segment pass skips these 8 records
+    } else if constexpr (SEG) {
         uint8_t* winw = reinterpret_cast<uint8_t*>(&win[gib][0]);
         if (mine) finish_gates<G, MODE, false, decltype(rd), 16 * WIN_CH, true, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane,
                                                                                           winw, wsA, wsB);
@@ -293,19 +306,8 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
             else *(GMEM u32x2*)dst = x;
         };
         if constexpr (STAGE) {
-            if (mine && lane == 0) {
-                uint64_t e = ~0ull;
-                if (wsA != ~0ull) {
-                    uint32_t f[3];
-                    emit_fields(g, f);
-                    auto fv = [&](uint32_t fo) -> uint64_t {
-                        return fo == NO_FIELD ? 0xffffull : (uint64_t)fo | ((uint64_t)((winb[hd + fo] << 8) | winb[hd + fo + 1]) << 32);
-                    };
-                    const uint64_t e0 = fv(f[0]), e1 = fv(f[1]);
-                    e = (e0 & 0xffffull) | ((e1 & 0xffffull) << 16) | (e0 >> 32 << 32) | (e1 >> 32 << 48);
-                }
-                __builtin_nontemporal_store(e, (GMEM uint64_t*)(p.stage + r));
-            }
+            if (mine && lane == 0) stage_record(p, r, wsA != ~0ull, g, winb, hd);
+            if (wl == 0) p.stage_flags[rw0 / R] = 1u;
         } else {
             if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
             if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
@@ -315,63 +317,74 @@ __global__ __launch_bounds__(256) void dwalk_kernel(KParams p) {
     }
 }
 
-// The segment pass of the staged descriptor-batch emit (variant 94): 8 lanes per record; a record
-// with an entry loads the 64-B segment(s) holding its fields (default cache policy), patches the
-// field bytes in and stores each segment whole, write-through and non-temporal (sc0 sc1 nt; a plain
-// or nt store after the default-policy load stays dirty on chip and is written back inside the next
-// read stream: tools/probe_wtax.hip, 0.054 against 0.106 ms per C2 pass).  Records anywhere in the
-// buffer: 64-bit addresses, so the store is written as the instruction (global_store_dwordx2 with its
-// cache-policy bits; a vector store).  The segments are the staging launch's decision (the whole-
-// segment rule of variant 61), so no two groups write one segment and no other write touches them.
+// The segment pass of the staged emit (variants 94; 80 / 81 in the experiments build): 8 lanes per
+// record; a record whose entry carries this launch pair's tag loads the 64-B segment(s) holding its
+// fields (default cache policy), patches the field bytes in and stores each segment whole,
+// write-through and non-temporal (sc0 sc1 nt; a plain or nt store after the default-policy load stays
+// dirty on chip and is written back inside the next read stream: tools/probe_wtax.hip, 0.054 against
+// 0.106 ms per C2 pass).  Records anywhere in the buffer: 64-bit addresses, so the store is written as
+// the instruction (global_store_dwordx2 with its cache-policy bits: a vector store).  The segments are
+// the staging launch's decision (its whole-segment rule), so no two groups write one segment and no
+// other write touches them.  A wavefront's 8 records (the staging launch's wavefront of 8, or part of
+// one) end at once when their flag says nothing was staged.
 __device__ __forceinline__ uint64_t patch_field(uint64_t x, int64_t k, uint32_t v) {
     if (k >= 0 && k < 8) x = (x & ~(0xffull << (8 * k))) | ((uint64_t)((v >> 8) & 0xffu) << (8 * k));
     if (k + 1 >= 0 && k + 1 < 8) x = (x & ~(0xffull << (8 * (k + 1)))) | ((uint64_t)(v & 0xffu) << (8 * (k + 1)));
     return x;
 }
 
-__global__ __launch_bounds__(256) void seg_pass_desc_kernel(KParams p) {
-    const uint64_t r = (uint64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+__global__ __launch_bounds__(1024) void seg_pass_kernel(KParams p) {
+    const uint64_t r = (uint64_t)blockIdx.x * 128 + (threadIdx.x >> 3);
     const int l = (int)(threadIdx.x & 7);
     if (r >= p.n) return;
+    if (p.stage_flags[r / 8] == 0u) return;  // (uniform over the wavefront's 8 records) nothing staged
     const uint64_t e = __builtin_nontemporal_load((const GMEM uint64_t*)(p.stage + r));
     if (e == ~0ull) return;
     const uint64_t off = p.desc ? *(const GMEM uint64_t*)((uint64_t)p.desc + 16 * r) : r * p.stride;
-    const uint32_t f0 = (uint32_t)(e & 0xffffu), f1 = (uint32_t)((e >> 16) & 0xffffu);
+    const uint32_t f0 = (uint32_t)(e & 0xffu), f1 = (uint32_t)((e >> 8) & 0xffu);
     const uint32_t v0 = (uint32_t)((e >> 32) & 0xffffu), v1 = (uint32_t)(e >> 48);
     const uint64_t a0 = (uint64_t)p.buf + off;
-    const uint32_t lo = min(f0 == 0xffffu ? 0xffffu : f0, f1 == 0xffffu ? 0xffffu : f1);
-    const uint32_t hi = max(f0 == 0xffffu ? 0u : f0 + 2, f1 == 0xffffu ? 0u : f1 + 2);
+    const uint32_t lo = min(f0 == 0xffu ? 0xffffu : f0, f1 == 0xffu ? 0xffffu : f1);
+    const uint32_t hi = max(f0 == 0xffu ? 0u : f0 + 2, f1 == 0xffu ? 0u : f1 + 2);
     const uint64_t sA = (a0 + lo) & ~63ull, sB = (a0 + hi - 1) & ~63ull;
     const uint64_t wA = sA + 8u * (uint32_t)l, wB = sB + 8u * (uint32_t)l;
     // both loads before either store (stores count in vmcnt with the loads, in order)
     uint64_t xa = *(const GMEM uint64_t*)wA;
     uint64_t xb = sB != sA ? *(const GMEM uint64_t*)wB : 0ull;
-    if (f0 != 0xffffu) xa = patch_field(xa, (int64_t)(a0 + f0) - (int64_t)wA, v0);
-    if (f1 != 0xffffu) xa = patch_field(xa, (int64_t)(a0 + f1) - (int64_t)wA, v1);
+    if (f0 != 0xffu) xa = patch_field(xa, (int64_t)(a0 + f0) - (int64_t)wA, v0);
+    if (f1 != 0xffu) xa = patch_field(xa, (int64_t)(a0 + f1) - (int64_t)wA, v1);
     asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(wA), "v"(xa) : "memory");
     if (sB != sA) {
-        if (f0 != 0xffffu) xb = patch_field(xb, (int64_t)(a0 + f0) - (int64_t)wB, v0);
-        if (f1 != 0xffffu) xb = patch_field(xb, (int64_t)(a0 + f1) - (int64_t)wB, v1);
+        if (f0 != 0xffu) xb = patch_field(xb, (int64_t)(a0 + f0) - (int64_t)wB, v0);
+        if (f1 != 0xffu) xb = patch_field(xb, (int64_t)(a0 + f1) - (int64_t)wB, v1);
         asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(wB), "v"(xb) : "memory");
     }
+}
+
+hipError_t launch_seg_pass(const KParams& p, hipStream_t s) {
+    // 1024-thread workgroups (128 records each): a chunk whose wavefronts mostly find nothing staged
+    // costs the dispatch of a quarter as many workgroups
+    hipLaunchKernelGGL(seg_pass_kernel, dim3((uint32_t)((p.n + 127) / 128)), dim3(1024), 0, s, p);
+    return hipGetLastError();
 }
 
 hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) {
 #ifndef SMOL_EXP
     // the product's forms: 63 (verify / emit), 41 (emit), 60 (verify)
     if (!(variant == 63 && (mode == MODE_VERIFY || mode == MODE_EMIT)) && !(variant == 60 && mode == MODE_VERIFY) &&
-        !(variant == 41 && mode == MODE_EMIT) && !(variant == 94 && mode == MODE_EMIT))
+        !(variant == 41 && mode == MODE_EMIT) && !(variant == 94 && mode == MODE_EMIT) && !(variant == 95 && mode == MODE_EMIT))
         return hipErrorInvalidValue;
 #endif
-    if (variant == 94 && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
-        if (!p.stage || p.n > kStageChunk) return hipErrorInvalidValue;
-        note_launch(KERN_DWALK, 94u, dwalk::G, dwalk::U);
+    if ((variant == 94 || variant == 95) && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
+        if (!p.stage || !p.stage_flags || p.n > kStageChunk) return hipErrorInvalidValue;
+        note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
         const uint32_t b = grid_blocks((p.n + dwalk::GPB - 1) / dwalk::GPB, kMaxGridBlocks);
-        hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27>), dim3(b), dim3(256), 0, s, p);
+        if (variant == 95)  // (experiments: held to 8 wavefronts per SIMD, 64 B of spills per lane)
+            hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27 | 32>), dim3(b), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27>), dim3(b), dim3(256), 0, s, p);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(seg_pass_desc_kernel, dim3((uint32_t)((p.n + 31) / 32)), dim3(256), 0, s, p);
-        return hipGetLastError();
+        return launch_seg_pass(p, s);
     }
     const uint64_t per = (uint64_t)dwalk::GPB;
     note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);

@@ -53,7 +53,8 @@ struct KParams {
     const uint8_t* addrs;  // 6LoWPAN NHC UDP batches: 32 B (IPv6 src, dst) per record, else nullptr
     uint32_t xcd_remap;    // walk kernel: 0 dispatch order; 1 block b takes the records of block
                            // xcd_block(b); K >= 2: those of xcd_chunk(b, K) (see below)
-    uint64_t* stage;       // staged emit (csum_xwalk.hip variant 80): one 8-B field entry per record
+    uint64_t* stage;       // staged emit (csum_walk.h stage_entry): one 8-B field entry per record
+    uint32_t* stage_flags; // staged emit: one flag per 8 records (1: their entries are this call's)
 };
 
 // The 8 XCDs of an MI355X are dealt workgroups round-robin (MI355X_MICROARCH.md, workgroup dispatch:
@@ -135,7 +136,9 @@ hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s);
 // the segment pass writes the field segments whole (csum_xwalk.hip).  Records per launch pair:
 constexpr uint64_t kStageChunk = 1ull << 21;
 inline bool staged_variant(int v) { return v == 80 || v == 81; }
-inline bool staged_desc_variant(int v) { return v == 94; }  // csum_dwalk.hip
+inline bool staged_desc_variant(int v) { return v == 94 || v == 95; }  // csum_dwalk.hip
+// The segment pass of the staged emit (csum_dwalk.hip seg_pass_kernel), after the staging launch.
+hipError_t launch_seg_pass(const KParams& p, hipStream_t s);
 
 // Synthetic batches and fault injection (tools; include/smolcsum_tools.h).
 struct SynthParams {

@@ -429,6 +429,30 @@ __device__ __forceinline__ void emit_fields(const Geom& g, uint32_t f[3]) {
     f[2] = g.in_off ? g.in_off + 10 : NO_FIELD;
 }
 
+// Staged emit (round 6; csum_dwalk.hip variant 94, csum_xwalk.hip variants 80 / 81): a record whose
+// field segments go out whole in the segment pass stages one 8-B entry: its two field offsets (< 256:
+// the fields lie in its LDS window; 0xff: none) and the two big-endian field values; every other
+// record of a staging wavefront writes ~0.  Each group of 8 consecutive records (one wavefront of the
+// segment pass) has a flag word: 1 when its entries were written by this call, 0 when none was (the
+// pass skips the group), so no entry of an earlier call is ever read.
+__device__ __forceinline__ uint64_t stage_entry(uint32_t f0, uint32_t v0, uint32_t f1, uint32_t v1) {
+    return (uint64_t)(f0 & 0xffu) | ((uint64_t)(f1 & 0xffu) << 8) | ((uint64_t)(v0 & 0xffffu) << 32) |
+           ((uint64_t)(v1 & 0xffffu) << 48);
+}
+// The entry of record r (its fields from the LDS window, where finish_gates patched them in), or ~0
+// when it is not staged; written by one lane.
+__device__ __forceinline__ void stage_record(const KParams& p, uint64_t r, bool staged, const Geom& g,
+                                             const uint8_t* winb, uint32_t hd) {
+    uint64_t e = ~0ull;
+    if (staged) {
+        uint32_t f[3];
+        emit_fields(g, f);
+        auto val = [&](uint32_t fo) { return fo == NO_FIELD ? 0u : (uint32_t)((winb[hd + fo] << 8) | winb[hd + fo + 1]); };
+        e = stage_entry(f[0] == NO_FIELD ? 0xffu : f[0], val(f[0]), f[1] == NO_FIELD ? 0xffu : f[1], val(f[1]));
+    }
+    __builtin_nontemporal_store(e, (GMEM uint64_t*)(p.stage + r));
+}
+
 // The gates of one record (MODE_EMIT / MODE_VERIFY / MODE_COPY), run by its whole group once every
 // lane holds its part `acc` of the aligned-word sum over [0, span_end): the header bytes the lanes
 // summed are taken out again, the IPv4 header sum and the pseudo-header address words are read from

@@ -88,8 +88,9 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // wavefront issues 12 loads instead of 16.
 // STAGE (variants 80 / 81, round 6; emit): the field segments are not written here.  A record whose
 // fields the whole segments cover (47's rule, all or nothing) stages one 8-B entry (its two field
-// offsets and values) in p.stage, and seg_pass_kernel writes the segments after this launch; any other
-// record writes its fields here as 2-B stores and stages none (entry ~0).  NTS = 32 (variant 80): the
+// offsets and values, csum_walk.h stage_entry) in p.stage, and the segment pass (csum_dwalk.hip
+// seg_pass_kernel) writes the segments after this launch; any other
+// record writes its fields here as 2-B stores and stages nothing.  NTS = 32 (variant 80): the
 // lanes of a record's first instruction that hold the segments of record offsets [10, 28) (an IPv4
 // record's two fields) load with the default cache policy, so that the segment pass finds those lines
 // on chip; 81: every load non-temporal.  Why (tools/probe_wtax.hip): field
@@ -335,19 +336,8 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
             else *(GMEM u32x2*)d = x;
         };
         if constexpr (STAGE) {
-            // the record's entry: field offsets (0xffff: none) and the values finish_gates patched
-            // into the window; ~0: nothing for the segment pass
-            if (mine && lane == 0) {
-                uint64_t e = ~0ull;
-                if (staged) {
-                    auto fv = [&](uint32_t fo) -> uint64_t {
-                        return fo == NO_FIELD ? 0xffffull : (uint64_t)fo | ((uint64_t)((winb[hd + fo] << 8) | winb[hd + fo + 1]) << 32);
-                    };
-                    const uint64_t e0 = fv(f[0]), e1 = fv(f[1]);
-                    e = (e0 & 0xffffull) | ((e1 & 0xffffull) << 16) | (e0 >> 32 << 32) | (e1 >> 32 << 48);
-                }
-                __builtin_nontemporal_store(e, (GMEM uint64_t*)(p.stage + r));
-            }
+            if (mine && lane == 0) stage_record(p, r, staged, g, winb, hd);
+            if (mine && lane == 0 && r % 8 == 0) p.stage_flags[r / 8] = 1u;  // every entry is written
         } else {
             if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
             if (wsB != ~0ull && lane < 8) seg_store(wsB + 8u * (uint32_t)lane);
@@ -361,58 +351,6 @@ __global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
     wave_lds_sync();  // the windows are rewritten by the next step
     tw = tn;
     }
-}
-
-// The segment pass of the staged emit (variants 80 / 81): 8 lanes per record, records in address
-// order; a record with an entry loads the 64-B segment(s) holding its fields (default cache policy: the
-// transposed walk left those lines on chip under variant 80), patches the field bytes in and stores
-// each segment whole, write-through and non-temporal (sc0 sc1 nt: tools/probe_wtax.hip measured
-// plain / nt stores after a default-policy load 35-40 ps per segment dearer; they stay dirty on chip
-// and are written back inside the next read stream).  The segments are those of the staging launch's
-// decision (47's race rule), so no two groups write one segment and no other write touches them.
-__device__ __forceinline__ uint64_t patch_be16(uint64_t x, int64_t k, uint32_t v) {
-    // bytes k (high) and k + 1 (low) of the 8-byte little-endian word x, where they fall inside it
-    if (k >= 0 && k < 8) x = (x & ~(0xffull << (8 * k))) | ((uint64_t)((v >> 8) & 0xffu) << (8 * k));
-    if (k + 1 >= 0 && k + 1 < 8) x = (x & ~(0xffull << (8 * (k + 1)))) | ((uint64_t)(v & 0xffu) << (8 * (k + 1)));
-    return x;
-}
-
-__global__ __launch_bounds__(256) void seg_pass_kernel(KParams p) {
-    const int wl = (int)(threadIdx.x & 63);
-    const uint64_t rw = (uint64_t)blockIdx.x * 32 + (uint64_t)((threadIdx.x & ~63u) >> 3);  // the wavefront's first record
-    if (rw >= p.n) return;
-    const uint64_t r = rw + (uint64_t)(wl >> 3);
-    const int l = wl & 7;
-    // one buffer resource per wavefront, based at its first record's first segment (8 records span
-    // at most 8 strides < 2^31 bytes: xwalk_fits)
-    const uint64_t base = ((uint64_t)p.buf + rw * p.stride) & ~63ull;
-    const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(base >> 32));
-    const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)bhi << 32) | blo), 0, 0x7fffffff, 0x00020000);
-    const uint64_t e = r < p.n ? __builtin_nontemporal_load((const GMEM uint64_t*)(p.stage + r)) : ~0ull;
-    if (e == ~0ull) return;
-    const uint32_t f0 = (uint32_t)(e & 0xffffu), f1 = (uint32_t)((e >> 16) & 0xffffu);
-    const uint32_t v0 = (uint32_t)((e >> 32) & 0xffffu), v1 = (uint32_t)(e >> 48);
-    const uint64_t a0 = (uint64_t)p.buf + r * p.stride;
-    const uint32_t lo = min(f0 == 0xffffu ? 0xffffu : f0, f1 == 0xffffu ? 0xffffu : f1);
-    const uint32_t hi = max(f0 == 0xffffu ? 0u : f0 + 2, f1 == 0xffffu ? 0u : f1 + 2);
-    const uint64_t sA = (a0 + lo) & ~63ull, sB = (a0 + hi - 1) & ~63ull;
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    // both segments' loads before either store (stores count in vmcnt with the loads, in order)
-    const uint64_t wA = sA + 8u * (uint32_t)l, wB = sB + 8u * (uint32_t)l;
-    const uint32_t oA = (uint32_t)(wA - base), oB = (uint32_t)(wB - base);
-    const u32x2 xa = __builtin_amdgcn_raw_buffer_load_b64(rs, oA, 0, 0);
-    const u32x2 xb = __builtin_amdgcn_raw_buffer_load_b64(rs, sB != sA ? oB : 0x80000000u, 0, 0);
-    auto patch = [&](u32x2 xv, uint64_t w) {
-        uint64_t x = (uint64_t)xv.x | ((uint64_t)xv.y << 32);
-        if (f0 != 0xffffu) x = patch_be16(x, (int64_t)(a0 + f0) - (int64_t)w, v0);
-        if (f1 != 0xffffu) x = patch_be16(x, (int64_t)(a0 + f1) - (int64_t)w, v1);
-        const u32x2 y = {(uint32_t)x, (uint32_t)(x >> 32)};
-        return y;
-    };
-    __builtin_amdgcn_raw_buffer_store_b64(patch(xa, wA), rs, oA, 0, 19 /* sc0 sc1 nt */);
-    if (sB != sA) __builtin_amdgcn_raw_buffer_store_b64(patch(xb, wB), rs, oB, 0, 19);
 }
 
 // records per wavefront for a record length (0: not served)
@@ -560,9 +498,8 @@ hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         if (e != hipSuccess) return e;
 #ifdef SMOL_EXP
         if (mode == MODE_EMIT && staged_variant(variant)) {
-            if (!q.stage || q.n > kStageChunk) return hipErrorInvalidValue;
-            hipLaunchKernelGGL(seg_pass_kernel, dim3((uint32_t)((q.n + 31) / 32)), dim3(256), 0, s, q);
-            e = hipGetLastError();
+            if (!q.stage || !q.stage_flags || q.n > kStageChunk) return hipErrorInvalidValue;
+            e = launch_seg_pass(q, s);
             if (e != hipSuccess) return e;
         }
 #endif
