@@ -35,7 +35,21 @@ struct smol_csum_ctx {
     void* stage_stream;
     bool stage_recorded;
     hipEvent_t stage_done;
+    // descriptor-batch emit chooses between the staged form (97) and the in-place one (41) from the
+    // previous staged call's wavefront flags (a sample of the first kSample copied to host memory):
+    // staged while at least half of the sampled wavefronts staged, else in place, probing with the
+    // staged form again every kReprobe calls
+    uint32_t* sample_host;    // pinned
+    hipEvent_t sample_ev;
+    bool sample_pending;
+    int desc_staged;          // 1: the staged form (also before any sample), 0: in place
+    uint32_t since_probe;
 };
+
+namespace {
+constexpr uint32_t kSample = 256;   // wavefront flags (8 records each) sampled per staged call
+constexpr uint32_t kReprobe = 64;   // in-place calls between two staged probes
+}
 
 namespace smolcsum {
 
@@ -176,7 +190,7 @@ int field_store_variant(int variant, bool has_desc) {
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62 || variant == 18) return 63;  // (63 stores 2-B fields only)
     if (variant == 20) return 60;
-    if (variant == 41 || variant == 94 || variant == 95) return 41;
+    if (variant == 41 || (variant >= 94 && variant <= 97)) return 41;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
@@ -188,11 +202,11 @@ int field_store_variant(int variant, bool has_desc) {
 bool variant_built(int v) {
     switch (v) {
         case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 41: case 44: case 47: case 57: case 60: case 63:
-        case 89: case 94: return true;
+        case 89: case 97: return true;
         default: break;
     }
 #ifdef SMOL_EXP
-    if ((v >= 80 && v <= 88) || v == 90 || v == 91 || v == 92 || v == 95) return true;
+    if ((v >= 80 && v <= 88) || v == 90 || v == 91 || v == 92 || (v >= 94 && v <= 96) || v == 98) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -248,7 +262,7 @@ struct Pick {
 // Variants that serve copy-emit only: copy_kernel (17, 21; 22 / 30 experiments), the transposed
 // layout (49-55, experiments) and the walk kernel's MODE_COPY forms 8 / 11 / 16 (experiments).  Forced
 // on a context, they leave emit / verify / data to the library's choice (the automatic dispatch).
-bool copy_only(int v) { return v == 8 || v == 11 || v == 16 || v == 17 || v == 21 || v == 22 || v == 30 || (v >= 49 && v <= 55); }
+bool copy_only(int v) { return v == 8 || v == 11 || v == 16 || v == 17 || v == 21 || v == 22 || v == 30 || v == 98 || (v >= 49 && v <= 55); }
 
 Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* b, const KParams& p) {
     const bool has_desc = b->desc != nullptr;
@@ -260,8 +274,8 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
         // (21; tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 / 17 stay selectable.
         const int cv = ctx->variant;
         if (cv >= 49 && cv <= 55 && xcopy_fits(p)) return {F_XCOPY, cv, -1};
-        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17 || cv == 22 || cv == 30) ? cv : 21;
-        const bool ck = var == 17 || var == 21 || var == 22 || var == 30;
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17 || cv == 22 || cv == 30 || cv == 98) ? cv : 21;
+        const bool ck = var == 17 || var == 21 || var == 22 || var == 30 || var == 98;
         const int gv = cv >= 0 ? cv : walk_variant(mode, has_desc);
         const int shape = ctx->shape >= 0 ? ctx->shape : ck ? (int)CFG_G16U4 : auto_shape(b->len, has_desc, line_grid(gv), gv);
         return {ck ? F_COPY : F_WALK, var, shape};
@@ -270,6 +284,8 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     if (variant < 0) {
         const int xv = nhc ? 0 : xwalk_auto(mode, b);
         variant = xv ? xv : auto_variant(mode, has_desc);
+        // descriptor-batch emit: the staged form while the records stage (see smol_csum_ctx)
+        if (variant == 41 && ctx->desc_staged) variant = 97;
     }
     if (mode == MODE_EMIT && (b->flags & SMOL_BATCH_FIELD_STORES)) variant = field_store_variant(variant, has_desc);
     // a kernel that does not serve the batch falls back to the default of its kind (descriptor emit:
@@ -295,15 +311,15 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     // 18 / 20 (non-temporal 2-B fields) in the experiments build, which also runs them forced over
     // fixed-stride batches
     if (mode == MODE_VERIFY) {
-        if (variant == 41 || variant == 18 || variant == 62 || variant == 94 || variant == 95) variant = 63;  // emit forms of 63
+        if (variant == 41 || variant == 18 || variant == 62 || (variant >= 94 && variant <= 97)) variant = 63;  // emit forms of 63
         if (variant == 20 || variant % 64 == 61) variant = 60;              // emit forms of 60
     }
 #ifdef SMOL_EXP
     const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63 ||
-                        variant == 18 || variant == 20 || variant == 41 || variant == 94 || variant == 95;
+                        variant == 18 || variant == 20 || variant == 41 || (variant >= 94 && variant <= 97);
     const bool dw_ok = (mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc;
 #else
-    const bool dw_var = variant == 60 || variant == 63 || variant == 41 || variant == 94;
+    const bool dw_var = variant == 60 || variant == 63 || variant == 41 || variant == 97;
     const bool dw_ok = (mode == MODE_VERIFY || (mode == MODE_EMIT && variant != 60)) && has_desc && !nhc;
 #endif
     if (dw_var) {
@@ -327,6 +343,44 @@ const char* family_kernel(const Pick& k) {
         case F_XCOPY: return "xcopy_kernel";
         default: return "csum_kernel";
     }
+}
+
+// The automatic descriptor-batch emit (nothing forced, IP records, 2-B-field mode not asked).
+bool has_desc_auto(const smol_csum_ctx_t* ctx, const smol_csum_batch_t* b, const uint8_t* d_addrs) {
+    return b->desc && !d_addrs && ctx->variant < 0 && !(b->flags & SMOL_BATCH_FIELD_STORES);
+}
+
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+// Before a descriptor-batch emit: take the last staged call's sample when it has arrived (a
+// non-blocking event query), and probe with the staged form every kReprobe in-place calls.
+void update_desc_choice(smol_csum_ctx_t* ctx, hipStream_t s) {
+    if (capturing(s)) return;  // a captured graph keeps the choice it was captured with
+    if (ctx->sample_pending && hipEventQuery(ctx->sample_ev) == hipSuccess) {
+        ctx->sample_pending = false;
+        uint32_t n = ctx->sample_host[kSample], staged = 0;
+        for (uint32_t i = 0; i < n && i < kSample; ++i) staged += ctx->sample_host[i] != 0u;
+        ctx->desc_staged = n == 0 || 2 * staged >= n ? 1 : 0;
+        ctx->since_probe = 0;
+    }
+    if (!ctx->desc_staged && !ctx->sample_pending && ++ctx->since_probe >= kReprobe) ctx->desc_staged = 1;
+}
+
+// After a staged descriptor-batch emit of n records: copy the first wavefront flags to host memory.
+void sample_desc_choice(smol_csum_ctx_t* ctx, uint64_t n, hipStream_t s) {
+    if (capturing(s) || ctx->sample_pending) return;
+    const uint32_t waves = (uint32_t)((n + 7) / 8 < kSample ? (n + 7) / 8 : kSample);
+    ctx->sample_host[kSample] = waves;
+    if (hipMemcpyAsync(ctx->sample_host, ctx->stage_flags, waves * sizeof(uint32_t), hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipEventRecord(ctx->sample_ev, s) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    ctx->sample_pending = true;
 }
 
 int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t* b,
@@ -378,6 +432,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
         }
         return SMOL_OK;
     }
+    const bool desc_auto = mode == MODE_EMIT && has_desc_auto(ctx, b, d_addrs);
+    if (desc_auto) update_desc_choice(ctx, s);
     const Pick k = pick_kernel(ctx, mode, b, p);
     if (mode == MODE_EMIT && ((k.family == F_XWALK && staged_variant(k.variant)) ||
                               (k.family == F_DWALK && staged_desc_variant(k.variant)))) {
@@ -399,7 +455,8 @@ int run(smol_csum_ctx_t* ctx, int mode, uint8_t* d_buf, const smol_csum_batch_t*
             const hipError_t e = k.family == F_DWALK ? launch_dwalk(mode, k.variant, q, s) : launch_xwalk(mode, k.variant, q, s);
             if (e != hipSuccess) return hip_fail(e, "checksum kernel launch");
         }
-        hipError_t er = hipEventRecord(ctx->stage_done, s);
+        if (desc_auto) sample_desc_choice(ctx, b->n < kStageChunk ? b->n : kStageChunk, s);
+        hipError_t er = hipEventRecord(ctx->stage_done, s);  // (after the sample's copy: it reads the flags)
         if (er != hipSuccess) return hip_fail(er, "hipEventRecord (staged emit)");
         ctx->stage_stream = stream;
         ctx->stage_recorded = true;
@@ -456,10 +513,15 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     e = hipMalloc(&stage, kStageChunk * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc(&flags, (kStageChunk / 8 + 64) * sizeof(uint32_t));
     if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    uint32_t* sample = nullptr;
+    hipEvent_t sev = nullptr;
+    if (e == hipSuccess) e = hipHostMalloc(&sample, (kSample + 1) * sizeof(uint32_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&sev, hipEventDisableTiming);
     if (e != hipSuccess) {
         (void)hipFree(dummy);
         if (stage) (void)hipFree(stage);
         if (flags) (void)hipFree(flags);
+        if (sample) (void)hipHostFree(sample);
         return hip_fail(e, "context allocation");
     }
     auto* c = new (std::nothrow) smol_csum_ctx;
@@ -468,6 +530,8 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
         (void)hipFree(stage);
         (void)hipFree(flags);
         (void)hipEventDestroy(done);
+        (void)hipHostFree(sample);
+        (void)hipEventDestroy(sev);
         return SMOL_ENOMEM;
     }
     c->dummy = dummy;
@@ -476,6 +540,11 @@ int smol_csum_ctx_create(int device, smol_csum_ctx_t** out) {
     c->stage_stream = nullptr;
     c->stage_recorded = false;
     c->stage_done = done;
+    c->sample_host = sample;
+    c->sample_ev = sev;
+    c->sample_pending = false;
+    c->desc_staged = 1;
+    c->since_probe = 0;
     c->tile_records = 32;
     c->max_blocks_set = false;
     c->xcd_remap = -1;
@@ -497,6 +566,9 @@ int smol_csum_ctx_destroy(smol_csum_ctx_t* ctx) {
         (void)hipFree(ctx->stage);
         (void)hipFree(ctx->stage_flags);
         (void)hipEventDestroy(ctx->stage_done);
+        if (ctx->sample_pending) (void)hipEventSynchronize(ctx->sample_ev);
+        (void)hipHostFree(ctx->sample_host);
+        (void)hipEventDestroy(ctx->sample_ev);
     }
     delete ctx;
     return SMOL_OK;

@@ -72,7 +72,9 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 // chunk stores, so that waiting for them does not also wait for those stores (gfx950 counts stores
 // in vmcnt, in issue order with the loads).
 // NTB (experiments build): bit 0 the body chunks stored non-temporal (variant 30), bit 1 also the
-// body's source chunks loaded non-temporal (variant 22).
+// body's source chunks loaded non-temporal (variant 22); bit 2 the destination chunks of the generic
+// (header / edge) chunks loaded non-temporal (variant 98, round 6: whether the 28-B header reads
+// then leave L2 as 64-B requests instead of whole 128-B lines).
 template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0, bool LBS = false, int NTB = 0>
 __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             const int lo = (int)rr.p0 - pos, hi = (int)rr.p1 - pos;
             const bool full = lo <= 0 && hi >= 16;
             const bool any = pay && lo < 16 && hi > 0;
-            d = ld16<false>((gcv4)(in && !(pay && full) ? base + 16ull * k : dummy));
+            d = ld16<(NTB & 4) != 0>((gcv4)(in && !(pay && full) ? base + 16ull * k : dummy));
             const uint64_t sA = (sk + 16ull * k) & ~15ull;
             const uint64_t a0 = sA < first ? first : sA > last ? last : sA;
             const uint64_t a1 = sA + 16 < first ? first : sA + 16 > last ? last : sA + 16;
@@ -320,7 +322,7 @@ hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    note_launch(KERN_COPY, NTB == 1 ? 30 : NTB == 3 ? 22 : LBS ? 21 : 17, G, U);
+    note_launch(KERN_COPY, NTB == 1 ? 30 : NTB == 3 ? 22 : NTB == 4 ? 98 : LBS ? 21 : 17, G, U);
     hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB, LBS, NTB>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
@@ -374,6 +376,9 @@ hipError_t launch_copy_nt(int var, const KParams& p, uint32_t max_blocks, hipStr
     if (var == 30)
         return im ? launch_copy2_one<true, 16, 4, 1, 2, true, 1>(p, max_blocks, s)
                   : launch_copy2_one<false, 16, 4, 1, 2, true, 1>(p, max_blocks, s);
+    if (var == 98)
+        return im ? launch_copy2_one<true, 16, 4, 1, 2, true, 4>(p, max_blocks, s)
+                  : launch_copy2_one<false, 16, 4, 1, 2, true, 4>(p, max_blocks, s);
     return im ? launch_copy2_one<true, 16, 4, 1, 2, true, 3>(p, max_blocks, s)
               : launch_copy2_one<false, 16, 4, 1, 2, true, 3>(p, max_blocks, s);
 }

@@ -59,7 +59,7 @@ constexpr uint32_t kStageMinBytes = 1024;  // STAGE: the wavefront's mean record
 // tools/probe_wtax.hip: field writes that land while a read stream runs cost 65-90 ps each, the same
 // segments loaded again and written in a pass of their own ~40 ps.
 template <int MODE, bool NOSTORE, bool GROUPS = false, int SEGF = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 32) ? 8 : 1))) void dwalk_kernel(KParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160) ? 8 : 1))) void dwalk_kernel(KParams p) {
     using namespace dwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
     __shared__ u32x4 win[GPB][WIN_CH];
@@ -83,6 +83,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 32)
         const uint64_t off = (rw0 + (uint64_t)wl) * p.stride;
         d = u32x4{(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)wl < cnt ? p.len : 0u, 0u};
     }
+    constexpr bool LITE = (SEGF & 64) != 0 && MODE == MODE_EMIT;
+    constexpr bool STAGE_ANY = (SEGF & 16) != 0 || LITE;
+    bool stage_wave = false;
+    if constexpr (STAGE_ANY) {
+        // from the descriptors in lanes 0 .. cnt - 1 (not the uniform arrays: they would stay live
+        // in SGPRs, 87 against 58, one wavefront per SIMD fewer): back to back, and their span
+        const uint64_t off = (uint64_t)d.x | ((uint64_t)d.y << 32), end = off + d.z;
+        const uint64_t pend = (uint64_t)(uint32_t)__shfl_up((int)(uint32_t)end, 1, 64) |
+                              ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(end >> 32), 1, 64) << 32);
+        const bool gap = (uint32_t)wl < cnt && wl != 0 && pend != off;
+        const uint64_t first = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)d.x) |
+                               ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)d.y) << 32);
+        const uint64_t last = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)cnt - 1) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(end >> 32), (int)cnt - 1) << 32);
+        stage_wave = __ballot(gap) == 0 && last - first >= (uint64_t)cnt * dwalk::kStageMinBytes;
+    }
     // wave-uniform record extents
     uint64_t A[R];
     uint32_t L[R];
@@ -103,6 +119,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 32)
     // ---- the windows: instruction w, lane l: record 4 w + l / 16, chunk l % 16 ----
     constexpr bool SEG = (SEGF & 1) != 0 && MODE == MODE_EMIT;
     constexpr bool STAGE = (SEGF & 16) != 0 && SEG;
+    // LITE (bit 6, variant 96): staged like STAGE, but the decision (just before the finish) keeps
+    // only its outcome and the field values go to the entry from finish_gates' registers (no window
+    // patch, no whole-segment addresses): variant 41's finish otherwise
     constexpr bool WNT = (SEGF & 2) == 0;
     const bool mine = (uint32_t)gw < cnt;
     const uint64_t r = rw0 + (uint64_t)gw;
@@ -153,7 +172,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 32)
     // desc_layouts_step_41_94.jsonl), staging every record: C3 packed step 1.598 -> 1.503 ms and
     // 500-3000-B records 0.703 -> 0.685, but 64-1500-B records 0.389 -> 0.467 and gapped / shuffled C3
     // +1 / +1.6 % (not back to back: few segments may go out whole)
-    const bool stage_wave = STAGE && contig && A[cnt - 1] + L[cnt - 1] - A[0] >= (uint64_t)cnt * dwalk::kStageMinBytes;
     if constexpr (SEG) {
       if (!STAGE || stage_wave) {
         uint32_t f[3], flo = NO_FIELD, fhi = 0;
@@ -289,8 +307,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 32)
             }
         }
     }
+    bool lite_staged = false;
+    if constexpr (LITE) {
+        if (stage_wave) {
+            // 61's whole-segment rule (below), all or nothing over the record's fields
+            uint32_t f[3], flo = NO_FIELD, fhi = 0;
+            emit_fields(g, f);
+            for (int j = 0; j < 3; ++j)
+                if (f[j] != NO_FIELD) {
+                    flo = f[j] < flo ? f[j] : flo;
+                    fhi = f[j] + 2 > fhi ? f[j] + 2 : fhi;
+                }
+            const bool ok_tail = mine && (fhi == 0 || fhi + 64 <= len);
+            const uint64_t okm = __ballot(lane == 0 && ok_tail);
+            if (mine && (g.fam == 4 || g.fam == 6) && fhi != 0 && ok_tail && f[2] == NO_FIELD) {
+                const bool prev_ok = gw != 0 && ((okm >> (uint32_t)(G * (gw - 1))) & 1ull);
+                const int32_t ph = (int32_t)(a0 & 63u);
+                const int32_t rA = ((ph + (int32_t)flo) & ~63) - ph, rB = ((ph + (int32_t)fhi - 1) & ~63) - ph;
+                const int32_t wend = 16 * WIN_CH - (int32_t)hd;
+                auto whole = [&](int32_t rel) { return rel + 64 <= wend && (rel >= 0 || prev_ok); };
+                lite_staged = rB <= rA + 64 && whole(rA) && (rB == rA || whole(rB));
+            }
+        }
+    }
     // ---- finish: the walk kernel's gates ----
-    if (STAGE && !stage_wave) {  // (wave-uniform) variant 41's finish, nothing staged
+    if constexpr (LITE) {
+        if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE, false, true>(p, g, a1, rd, winb, hd, a0, r, lane,
+                                                                                            nullptr, ~0ull, ~0ull,
+                                                                                            !stage_wave ? 0 : lite_staged ? 1 : 2);
+        if (wl == 0) p.stage_flags[rw0 / R] = stage_wave ? 1u : 0u;
+    } else if (STAGE && !stage_wave) {  // (wave-uniform) variant 41's finish, nothing staged
         if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, a1, rd, winb, hd, a0, r, lane);
         if (wl == 0) p.stage_flags[rw0 / R] = 0u;  // the segment pass skips these 8 records
     } else if constexpr (SEG) {
@@ -372,14 +418,19 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
 #ifndef SMOL_EXP
     // the product's forms: 63 (verify / emit), 41 (emit), 60 (verify)
     if (!(variant == 63 && (mode == MODE_VERIFY || mode == MODE_EMIT)) && !(variant == 60 && mode == MODE_VERIFY) &&
-        !(variant == 41 && mode == MODE_EMIT) && !(variant == 94 && mode == MODE_EMIT) && !(variant == 95 && mode == MODE_EMIT))
+        !(variant == 41 && mode == MODE_EMIT) && !(variant == 94 && mode == MODE_EMIT) && !(variant == 95 && mode == MODE_EMIT) &&
+        !(variant == 96 && mode == MODE_EMIT) && !(variant == 97 && mode == MODE_EMIT))
         return hipErrorInvalidValue;
 #endif
-    if ((variant == 94 || variant == 95) && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
+    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97) && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
         if (!p.stage || !p.stage_flags || p.n > kStageChunk) return hipErrorInvalidValue;
         note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
         const uint32_t b = grid_blocks((p.n + dwalk::GPB - 1) / dwalk::GPB, kMaxGridBlocks);
-        if (variant == 95)  // (experiments: held to 8 wavefronts per SIMD, 64 B of spills per lane)
+        if (variant == 96)  // held to 8 wavefronts per SIMD (12 B of spills per lane; 97: 7, none)
+            hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 128>), dim3(b), dim3(256), 0, s, p);
+        else if (variant == 97)
+            hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64>), dim3(b), dim3(256), 0, s, p);
+        else if (variant == 95)  // (experiments: held to 8 wavefronts per SIMD, 64 B of spills per lane)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27 | 32>), dim3(b), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27>), dim3(b), dim3(256), 0, s, p);
         hipError_t e = hipGetLastError();

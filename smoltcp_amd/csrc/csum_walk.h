@@ -462,12 +462,16 @@ __device__ __forceinline__ void stage_record(const KParams& p, uint64_t r, bool 
 // SEGP (fixed-stride emit, SEGW): the 64-B segments wsA / wsB (~0: none) go out whole from the
 // window afterwards; a field is patched into the window, and stored to global memory unless both
 // of its bytes lie in those segments.
+// STG (staged emit, csum_dwalk.hip variant 96): `stg` 1 writes the record's field values to its staged
+// entry instead of the record (the caller has decided its segments go out whole in the segment pass:
+// no third field, both fields inside the LDS window); 2 stores the fields here and writes the entry
+// ~0; 0 stores them here (a wavefront that stages nothing).
 template <int G, int MODE, bool NHC, class RD, int WINB = 0, bool SEGP = false, bool NOSTORE = false,
-          bool NTST = false>
+          bool NTST = false, bool STG = false>
 __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, uint32_t acc, const RD& rd,
                                              const uint8_t* winb, uint32_t head, uint64_t a0, uint64_t r,
                                              int lane, uint8_t* winw = nullptr, uint64_t wsA = ~0ull,
-                                             uint64_t wsB = ~0ull) {
+                                             uint64_t wsB = ~0ull, int stg = 0) {
     constexpr bool EMITS = MODE == MODE_EMIT || MODE == MODE_COPY;
     const bool odd = (a0 & 1u) != 0;
     // Header bytes [0, l4_off) that the lanes summed (taken out of the L4 sum), the IPv4
@@ -628,10 +632,16 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
             if (fl4 != MF_NONE) put(fl4, vl4);
             if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
         } else if (EMITS) {
-            if (fip != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fip, vip);
-            if (fin != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fin, vin);
-            if (fl4 != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fl4, vl4);
-            if (NHC && nb0 != NO_FIELD) wrec[0] = (uint8_t)nb0;
+            if (STG && stg == 1) {
+                const uint64_t e = stage_entry(fip == MF_NONE ? 0xffu : fip, vip, fl4 == MF_NONE ? 0xffu : fl4, vl4);
+                __builtin_nontemporal_store(e, (GMEM uint64_t*)(p.stage + r));
+            } else {
+                if (fip != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fip, vip);
+                if (fin != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fin, vin);
+                if (fl4 != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fl4, vl4);
+                if (NHC && nb0 != NO_FIELD) wrec[0] = (uint8_t)nb0;
+                if (STG && stg == 2) __builtin_nontemporal_store(~0ull, (GMEM uint64_t*)(p.stage + r));
+            }
             if (p.status) ((gu8)p.status)[r] = (uint8_t)st;
         } else {
             const bool mal = (st & SMOL_ST_MALFORMED) != 0;
@@ -1456,6 +1466,7 @@ hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks
         case 21: return launch_copy_v21(shape, p, max_blocks, s);
 #ifdef SMOL_EXP
         case 30:
+        case 98:
         case 22: return launch_copy_nt(var, p, max_blocks, s);
         case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
         case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);

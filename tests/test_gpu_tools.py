@@ -6,10 +6,12 @@ import pytest
 import torch
 
 from smoltcp_amd import engine as E
+from tests import pktgen as P
 from tests.dispatch_table import fixed_launch
 from tests.engines import VariantEngine
 
 pytestmark = pytest.mark.gpu
+CAPS = (0, 0, 0, 0, 0)
 
 
 @pytest.fixture(scope="module")
@@ -90,10 +92,15 @@ def test_last_launch_families(eng):
     offs = np.arange(n, dtype=np.uint64) * L
     bd = E.Batch.from_records(offs, np.full(n, L, np.uint32), E.KIND_IP, "cuda:0")
     # descriptor batches: the per-group descriptor walk (csum_dwalk.hip, cached header windows),
-    # 8 lanes x 4 chunks, both operations; the tile kernel when forced (variant 7)
-    eng.emit(buf, bd)
-    ll = eng.last_launch()
-    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 41, 8, 4), ll
+    # 8 lanes x 4 chunks, both operations (emit staged on a fresh context: 97); the tile kernel when
+    # forced (variant 7)
+    e2 = VariantEngine(0)
+    try:
+        e2.emit(buf, bd)
+        ll = e2.last_launch()
+    finally:
+        e2.close()
+    assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 97, 8, 4), ll
     eng.verify(buf, bd)
     ll = eng.last_launch()
     assert (ll["kernel"], ll["variant"], ll["G"], ll["U"]) == ("dwalk_kernel", 63, 8, 4), ll
@@ -183,3 +190,49 @@ def test_segment_probe_changes_nothing(eng, nt):
     eng.segment_probe(d, bitmap, nt=nt)
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy(), host)
+
+
+def test_descriptor_emit_choice_follows_the_records(eng):
+    """Descriptor-batch emit picks the staged form (97) or the in-place one (41) from the previous staged
+    call's sample of wavefront flags (csum_api.cpp update_desc_choice): short records (no wavefront
+    stages) switch a fresh context to 41 after one call, long back-to-back records keep 97; both
+    forms write the oracle's bytes."""
+    import oracle
+
+    rng = np.random.default_rng(97)
+    e = VariantEngine(0)
+    try:
+        def batch_of(lo, hi, n):
+            lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
+            offs = np.zeros(n, dtype=np.uint64)
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+            total = int(offs[-1] + lens[-1]) + 16
+            buf = torch.zeros(total, dtype=torch.uint8, device="cuda:0")
+            b = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0")
+            e.synth(buf, b, E.SYNTH_TCP4, seed=int(lo))
+            return buf, b, offs, lens
+
+        def run(buf, b, offs, lens):
+            host = buf.cpu().numpy().copy()
+            e.emit(buf, b)
+            torch.cuda.synchronize()
+            ll = e.last_launch()
+            ref = host.copy()
+            oracle.batch_emit(ref, P.oracle_desc(offs, lens, E.KIND_IP), len(offs), 0, 0, E.KIND_IP, CAPS)
+            assert np.array_equal(buf.cpu().numpy(), ref)
+            return ll["variant"]
+
+        short = batch_of(64, 300, 20000)
+        assert run(*short) == 97  # a fresh context stages (no sample yet)
+        assert run(*short) == 41  # nothing staged in the sample: in place
+        assert e.kernel_for("emit", short[1]) == "dwalk_kernel"
+        long_ = batch_of(3000, 9000, 4000)
+        assert run(*long_) == 41  # (the decision of the last sample)
+        for _ in range(70):  # the staged probe every 64 in-place calls, which then sticks
+            v = run(*long_)
+            if v == 97:
+                break
+        assert v == 97
+        assert run(*long_) == 97
+    finally:
+        e.close()
