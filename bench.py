@@ -513,7 +513,10 @@ def parity_spread(E, wl, records: int = 65536, windows: int = 64) -> dict:
     runs of consecutive records, evenly spaced from the first record to the last): the oracle's emit of
     each run (emit is idempotent) must reproduce the device's emitted TX bytes, and its verify of the
     RX bytes the device's status bytes, bit for bit.  Runs on every config, with or without the CPU
-    baseline (whose sample is the batch's first 1.6 GB)."""
+    baseline (whose sample is the batch's first 1.6 GB).  C2copy: the TX bytes are the fused
+    copy-emit's; the oracle's copy + emit of each run (the payload copied from the source, then the
+    fields) must reproduce them, so a wrong payload byte or field fails it (header bytes other than
+    the fields are the oracle's input, not checked)."""
     import oracle
 
     n = wl.n
@@ -522,6 +525,7 @@ def parity_spread(E, wl, records: int = 65536, windows: int = 64) -> dict:
     desc_all = wl.batch.desc.cpu().numpy().view(E.DESC_DTYPE) if wl.batch.desc is not None else None
     stride, L = (wl.batch.stride, wl.batch.length) if desc_all is None else (0, 0)
     st_all = wl.status.cpu().numpy()
+    copy_all = wl.copy.cpu().numpy().view(E.COPY_DTYPE) if wl.copy is not None else None
     checked, emit_ok, verify_ok = 0, True, True
     for lo in starts:
         hi = min(n, lo + per)
@@ -535,7 +539,15 @@ def parity_spread(E, wl, records: int = 65536, windows: int = 64) -> dict:
         tx = wl.tx[a:b].cpu().numpy()
         rx = wl.rx[a:b].cpu().numpy()
         ref = tx.copy()
-        oracle.batch_emit(ref, d, hi - lo, stride, L, wl.kind, (0, 0, 0, 0, 0))
+        if copy_all is None:
+            oracle.batch_emit(ref, d, hi - lo, stride, L, wl.kind, (0, 0, 0, 0, 0))
+        else:
+            cp = copy_all[lo:hi].copy()
+            s0 = int(cp["src_offset"].min())
+            s1 = int((cp["src_offset"] + cp["len"].astype(np.uint64)).max())
+            cp["src_offset"] -= np.uint64(s0)
+            src = wl.src[s0:s1].cpu().numpy()
+            oracle.batch_copy_emit(ref, d, hi - lo, src, cp, stride, L, wl.kind, (0, 0, 0, 0, 0))
         emit_ok &= bool(np.array_equal(ref, tx))
         st = oracle.batch_verify(rx.copy(), d, hi - lo, stride, L, wl.kind, (0, 0, 0, 0, 0))
         verify_ok &= bool(np.array_equal(st, st_all[lo:hi]))
@@ -543,8 +555,9 @@ def parity_spread(E, wl, records: int = 65536, windows: int = 64) -> dict:
     return {"records": checked, "windows": len(starts), "emit_bitexact": emit_ok, "verify_bitexact": verify_ok,
             "checker": "oracle/csum_oracle.c",
             "sample": f"{len(starts)} runs of {per} consecutive records evenly spaced over all {n} records "
-                      f"(first run at record 0, last ending at record {n - 1}): emit of TX batch 0, verify of RX "
-                      f"batch 0 (the last verify's status)"}
+                      f"(first run at record 0, last ending at record {n - 1}): "
+                      + ("the fused copy-emit's TX bytes" if copy_all is not None else "emit of TX batch 0")
+                      + ", verify of RX batch 0 (the last verify's status)"}
 
 
 def _launch_name(ll):
@@ -829,7 +842,7 @@ def main(argv=None):
     cpu, parity = None, None
     if rank == 0 and world == 1 and wl.copy is None:
         cpu, parity = cpu_baseline(E, wl, args.cpu_seconds)
-    if rank == 0 and wl.copy is None:
+    if rank == 0:
         spread = parity_spread(E, wl)
         parity = dict(parity or {}, spread=spread) if parity else {"spread": spread}
 

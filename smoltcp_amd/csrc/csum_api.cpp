@@ -206,7 +206,7 @@ bool variant_built(int v) {
         default: break;
     }
 #ifdef SMOL_EXP
-    if ((v >= 80 && v <= 88) || v == 90 || v == 91 || v == 92 || (v >= 94 && v <= 96) || v == 98) return true;
+    if ((v >= 80 && v <= 96 && v != 89) || v == 98 || v == 99) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -301,7 +301,8 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     const int v64 = variant % 64;
     const bool xw_var = (variant < 64 && (variant == 44 || variant == 47 || variant == 43 || variant == 45 || variant == 46 ||
                                           variant == 15 || variant == 48 || variant == 57 || variant == 58 || variant == 59)) ||
-                        (variant >= 64 && (v64 == 44 || v64 == 47)) || staged_variant(variant) || (variant >= 82 && variant <= 92);
+                        (variant >= 64 && (v64 == 44 || v64 == 47)) || staged_variant(variant) || (variant >= 82 && variant <= 93) ||
+                        variant == 99;
     if (xw_var) {
         if ((mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc && xwalk_fits(p)) return {F_XWALK, variant, -1};
         variant = fallback;

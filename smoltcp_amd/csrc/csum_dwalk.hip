@@ -363,8 +363,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160
     }
 }
 
-// The segment pass of the staged emit (variants 94; 80 / 81 in the experiments build): 8 lanes per
-// record; a record whose entry carries this launch pair's tag loads the 64-B segment(s) holding its
+// The segment pass of the staged emit (variant 97, the product's descriptor-batch emit; 94-96 and
+// 80 / 81 in the experiments build): 8 lanes per record; on a wavefront of 8 records whose flag the
+// staging launch set, a record with a staged entry (not ~0) loads the 64-B segment(s) holding its
 // fields (default cache policy), patches the field bytes in and stores each segment whole,
 // write-through and non-temporal (sc0 sc1 nt; a plain or nt store after the default-policy load stays
 // dirty on chip and is written back inside the next read stream: tools/probe_wtax.hip, 0.054 against

@@ -429,7 +429,7 @@ __device__ __forceinline__ void emit_fields(const Geom& g, uint32_t f[3]) {
     f[2] = g.in_off ? g.in_off + 10 : NO_FIELD;
 }
 
-// Staged emit (round 6; csum_dwalk.hip variant 94, csum_xwalk.hip variants 80 / 81): a record whose
+// Staged emit (round 6; csum_dwalk.hip variants 94-97, csum_xwalk.hip variants 80 / 81): a record whose
 // field segments go out whole in the segment pass stages one 8-B entry: its two field offsets (< 256:
 // the fields lie in its LDS window; 0xff: none) and the two big-endian field values; every other
 // record of a staging wavefront writes ~0.  Each group of 8 consecutive records (one wavefront of the
@@ -462,7 +462,7 @@ __device__ __forceinline__ void stage_record(const KParams& p, uint64_t r, bool 
 // SEGP (fixed-stride emit, SEGW): the 64-B segments wsA / wsB (~0: none) go out whole from the
 // window afterwards; a field is patched into the window, and stored to global memory unless both
 // of its bytes lie in those segments.
-// STG (staged emit, csum_dwalk.hip variant 96): `stg` 1 writes the record's field values to its staged
+// STG (staged emit, csum_dwalk.hip variants 96 / 97): `stg` 1 writes the record's field values to its staged
 // entry instead of the record (the caller has decided its segments go out whole in the segment pass:
 // no third field, both fields inside the LDS window); 2 stores the fields here and writes the entry
 // ~0; 0 stores them here (a wavefront that stages nothing).

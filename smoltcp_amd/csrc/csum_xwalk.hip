@@ -97,8 +97,8 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // writes that land while a read stream runs cost 65-77 ps each, the same writes in a pass of their own
 // ~20 ps.
 template <int MODE, int R, bool NOSTORE, bool SEG, bool PERSIST = false, int NTS = 0, bool HALF = false,
-          bool STAGE = false, int HINT = 0>
-__global__ __launch_bounds__(256) void xwalk_kernel(KParams p) {
+          bool STAGE = false, int HINT = 0, int WPE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void xwalk_kernel(KParams p) {
     using namespace xwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
     constexpr int G = 64 / R;    // lanes per record
@@ -374,6 +374,16 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else if (variant == 83) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if (variant == 93 || variant == 99) {  // round 6: 89 / 57 held to 5 (93) or 6 (99) wavefronts per SIMD
+        if (variant == 93) {
+            if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7, 5>), dim3(blocks), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 0, 5>), dim3(blocks), dim3(256), 0, s, p);
+        } else {
+            if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7, 6>), dim3(blocks), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 0, 6>), dim3(blocks), dim3(256), 0, s, p);
+        }
         return;
     }
     if (variant >= 90 && variant <= 92) {  // verify hint forms 8-10 (emit: 57)

@@ -101,6 +101,20 @@ def test_bench_gpu_contract():
 
 
 @pytest.mark.gpu
+def test_bench_c2copy_parity_spread():
+    """C2copy's line carries the oracle check too: the fused copy-emit's TX bytes (payload and
+    fields) over runs of records spread across the whole batch."""
+    r = _run(["--gpus", "1", "--config", "c2copy", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0",
+              "--ramp-ms", "50"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    sp = d["parity_sample"]["spread"]
+    assert sp["emit_bitexact"] and sp["verify_bitexact"] and sp["records"] >= 65536
+    assert "copy-emit" in sp["sample"]
+    assert d["kernels_launched"]["copy_emit"].startswith("copy_kernel")
+
+
+@pytest.mark.gpu
 def test_bench_under_torchrun_rccl():
     """The driver's N > 1 launch (torch.distributed.run, one rank per GPU) at the size a one-GPU
     box allows: one rank, with the RCCL process group, barriers, max-over-ranks all_reduce and

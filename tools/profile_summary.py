@@ -37,6 +37,8 @@ def kernel_role(name: str):
     """'emit' / 'verify' / 'data' for the checksum kernels, else None."""
     if re.search(r"copy_kernel<", name):  # csum_copy.hip: <G, U, IMPLICIT>, copy-emit only
         return "copy_emit"
+    if "seg_pass_kernel" in name:  # csum_dwalk.hip: the staged emit's second launch
+        return "emit_seg_pass"
     m = re.search(r"[xd]walk_kernel<([^>]*)>", name)  # csum_xwalk.hip <MODE, R, ...>, csum_dwalk.hip <MODE, ...>
     if m:
         return MODES.get(m.group(1).split(",")[0].strip())
@@ -102,6 +104,15 @@ def main():
         if role in avg_ns:
             cfg[role]["kernel_trace_avg_ns"] = avg_ns[role][1]
             cfg[role]["kernel_trace_calls"] = avg_ns[role][2]
+    if "emit" in cfg and "emit_seg_pass" in cfg:
+        # staged emit (round 6): one emit call = the staging launch + the segment pass; "emit" is their
+        # sum (what bench.py's HIP events around the call time), the parts stay beside it
+        st, sp = cfg["emit"], cfg["emit_seg_pass"]
+        cfg["emit_staging"] = st
+        cfg["emit"] = {"kernel": st["kernel"] + " + seg_pass_kernel",
+                       **{k: st[k] + sp[k] for k in ("hbm_bytes_per_launch", "read_bytes_corrected", "write_bytes")}}
+        if "kernel_trace_avg_ns" in st and "kernel_trace_avg_ns" in sp:
+            cfg["emit"]["kernel_trace_avg_ns"] = st["kernel_trace_avg_ns"] + sp["kernel_trace_avg_ns"]
     doc[a.config] = cfg
     doc["method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                      "`python3 bench.py --config <cfg> --steps 5 --warmup 1 --ramp-ms 0 --cpu-seconds 0`; counters in KB "
