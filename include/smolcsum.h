@@ -218,7 +218,8 @@ int smol_csum_batch_data(smol_csum_ctx_t* ctx, const uint8_t* d_buf,
  * ~17 MB of device scratch, allocated by smol_csum_ctx_create, and orders a staged emit issued on
  * another stream after the previous one (an event wait), so emits on one context may use several
  * streams.  No device memory is allocated by a batched call: the calls may be captured in a HIP
- * graph. */
+ * graph (a graph holding a staged emit uses the context's scratch when it replays: do not replay it
+ * concurrently with another emit on the same context). */
 int smol_csum_batch_emit(smol_csum_ctx_t* ctx, uint8_t* d_buf, const smol_csum_batch_t* batch,
                          const smol_checksum_caps_t* caps, uint8_t* d_status, void* stream);
 
