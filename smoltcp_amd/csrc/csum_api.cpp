@@ -150,9 +150,10 @@ int auto_variant(int mode, bool has_desc) {
 // (profiles/r06_dispatch_sweep_box{1,2,3}.jsonl), turned into dispatch_table.inc by
 // tools/gen_dispatch_table.py (the least summed time per entry).  Verify: the walk kernel (5), the
 // transposed walk (47) or 47 with the first-load hint (89: lanes 0-3 of each record's first instruction
-// with the default cache policy; C2 verify 0.2342 -> 0.2259 ms); emit: the walk kernel (39), 47 or 57 (47
-// with non-temporal field segments).  Outside 1024 .. 9023 B the walk kernel (round 5: past 9000 B the
-// two trade places by length, within 2 %).
+// with the default cache policy; C2 verify 0.2342 -> 0.2259 ms); emit: the walk kernel (39), 47 or, where
+// the sweep measured 57 (47 with non-temporal field segments) fastest, 101 (57's segments stored
+// write-through: C2 / C4 emit 1-1.7 % below 57, late round 6).  Outside 1024 .. 9023 B the walk kernel
+// (round 5: past 9000 B the two trade places by length, within 2 %).
 // Returns the transposed-walk variant to run (0: the walk kernel).
 #include "dispatch_table.inc"
 
@@ -163,7 +164,7 @@ int xwalk_auto(int mode, const smol_csum_batch_t* b) {
     const int col = b->stride != b->len ? 2 : (b->len % 64 == 0 ? 0 : 1);
     const char c = (mode == MODE_VERIFY ? kVerifyTable : kEmitTable)[k][col];
     if (mode == MODE_VERIFY) return c == 'h' ? 89 : c == 'x' ? 47 : 0;
-    return c == 'n' ? 57 : c == 'x' ? 47 : 0;
+    return c == 'n' ? 101 : c == 'x' ? 47 : 0;
 }
 
 // The XCD block order (csum_launch.h xcd_block / xcd_chunk) when none is forced: the contiguous order
@@ -186,7 +187,9 @@ int xcd_remap_auto(int mode, const smol_csum_batch_t* b) {
 // SMOL_BATCH_FIELD_STORES: the same kernel without the whole-segment writes (2-B field stores only).
 int field_store_variant(int variant, bool has_desc) {
     if (variant == 19 || variant == 23 || variant == 24 || variant == 25 || variant == 29 || variant == 39) return 5;
-    if (variant == 47 || variant == 57 || variant == 45 || (variant >= 80 && variant <= 92)) return 44;
+    if (variant == 47 || variant == 57 || variant == 45 || (variant >= 80 && variant <= 93) || variant == 99 || variant == 100 ||
+        variant == 101)
+        return 44;
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62 || variant == 18) return 63;  // (63 stores 2-B fields only)
     if (variant == 20) return 60;
@@ -202,11 +205,11 @@ int field_store_variant(int variant, bool has_desc) {
 bool variant_built(int v) {
     switch (v) {
         case -1: case 5: case 7: case 13: case 17: case 21: case 39: case 41: case 44: case 47: case 57: case 60: case 63:
-        case 89: case 97: return true;
+        case 89: case 97: case 101: return true;
         default: break;
     }
 #ifdef SMOL_EXP
-    if ((v >= 80 && v <= 96 && v != 89) || v == 98 || v == 99) return true;
+    if ((v >= 80 && v <= 96 && v != 89) || (v >= 98 && v <= 100)) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -302,7 +305,7 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     const bool xw_var = (variant < 64 && (variant == 44 || variant == 47 || variant == 43 || variant == 45 || variant == 46 ||
                                           variant == 15 || variant == 48 || variant == 57 || variant == 58 || variant == 59)) ||
                         (variant >= 64 && (v64 == 44 || v64 == 47)) || staged_variant(variant) || (variant >= 82 && variant <= 93) ||
-                        variant == 99;
+                        variant == 99 || variant == 100 || variant == 101;
     if (xw_var) {
         if ((mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc && xwalk_fits(p)) return {F_XWALK, variant, -1};
         variant = fallback;

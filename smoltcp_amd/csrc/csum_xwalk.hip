@@ -86,6 +86,10 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // HALF (variant 59, experiments build; R = 8, records of at most 1409 B, whose line-grid span fits
 // 96 chunks): a record's second KiB is half an instruction, two records per instruction, so a
 // wavefront issues 12 loads instead of 16.
+// NTS = 65 (variant 101, the product's emit where the dispatch table says 'n', since late round 6): the
+// segments stored with sc1 nt, write-through and non-temporal (the staged emit's segment-pass policy,
+// here inside the stream), as a vector store written as the instruction; NTS = 64 (variant 100,
+// experiments build): sc0 sc1 nt.
 // STAGE (variants 80 / 81, round 6; emit): the field segments are not written here.  A record whose
 // fields the whole segments cover (47's rule, all or nothing) stages one 8-B entry (its two field
 // offsets and values, csum_walk.h stage_entry) in p.stage, and the segment pass (csum_dwalk.hip
@@ -332,6 +336,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
         auto seg_store = [&](uint64_t d) {
             const u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - wb));
             if constexpr (NOSTORE) asm volatile("" ::"v"(x), "v"(d));
+            else if constexpr (NTS == 64)  // (variant 100) write-through non-temporal vector store
+                asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(d), "v"(x) : "memory");
+            else if constexpr (NTS == 65)  // (variant 101) sc1 nt
+                asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(d), "v"(x) : "memory");
             else if (nts) __builtin_nontemporal_store(x, (GMEM u32x2*)d);
             else *(GMEM u32x2*)d = x;
         };
@@ -374,6 +382,11 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else if (variant == 83) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if (variant == 100) {  // round 6: 57 with the segments stored sc0 sc1 nt (101: sc1 nt, the product's); verify: 89
+        if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 64>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
     if (variant == 93 || variant == 99) {  // round 6: 89 / 57 held to 5 (93) or 6 (99) wavefronts per SIMD
@@ -457,13 +470,13 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #endif
-    const bool seg = variant % 64 == 47 || variant == 57 || variant == 89;
-    if (mode == MODE_VERIFY) {  // (57: 47's verify)
+    const bool seg = variant % 64 == 47 || variant == 57 || variant == 89 || variant == 101;
+    if (mode == MODE_VERIFY) {  // (57: 47's verify; 101: 89's)
         // 89 (round 6): lanes 0-3 of each record's first instruction (the first 64 B of its first line)
         // load with the default cache policy, the rest non-temporal: C2 verify 0.2342 -> 0.2259 ms
         // (bench lines interleaved on one box, profiles/r06_experiments/verify_hint_ab.txt); the split
         // itself without the policy change (90) gains nothing
-        if (variant == 89) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7>), dim3(blocks), dim3(256), 0, s, p);
+        if (variant == 89 || variant == 101) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7>), dim3(blocks), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
@@ -474,7 +487,11 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #endif
-    if (variant == 57 || variant == 89) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+    // 101 (late round 6): 57's segments stored write-through (sc1 nt): C2 emit 0.3089-0.3102 ->
+    // 0.3061-0.3064 ms, C4 0.2728-0.2739 -> 0.2682-0.2689 ms (bench lines interleaved on one box,
+    // profiles/r06_experiments/writethrough_segments_ab.txt)
+    if (variant == 101) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 65>), dim3(blocks), dim3(256), 0, s, p);
+    else if (variant == 57 || variant == 89) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1>), dim3(blocks), dim3(256), 0, s, p);
     else if (seg) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true>), dim3(blocks), dim3(256), 0, s, p);
     else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, false>), dim3(blocks), dim3(256), 0, s, p);
 }

@@ -145,7 +145,7 @@ def test_variant_lists():
 
     L = _lib.lib()
     built = [v for v in range(-1, 128) if L.smol_csum_tool_variant_built(v)]
-    assert built == [-1, 5, 7, 13, 17, 21, 39, 41, 44, 47, 57, 60, 63, 89, 97], built
+    assert built == [-1, 5, 7, 13, 17, 21, 39, 41, 44, 47, 57, 60, 63, 89, 97, 101], built
     if os.path.exists(_lib.EXP_LIB_PATH):
         X = _lib.lib(_lib.EXP_LIB_PATH)
         exp = {v for v in range(-1, 128) if X.smol_csum_tool_variant_built(v)}
@@ -156,7 +156,7 @@ def test_dispatch_table_matches_sweeps():
     """smoltcp_amd/csrc/dispatch_table.inc (the fixed-stride dispatch, csum_api.cpp xwalk_auto) is what
     tools/gen_dispatch_table.py makes from the committed length sweeps (profiles/r06_dispatch_sweep_*),
     and C2's 1500-B records take the transposed walk with the first-load hint (verify) and with
-    non-temporal segments (emit)."""
+    non-temporal write-through segments (emit, 101: the sweep's 57 with write-through stores)."""
     import subprocess
 
     from tests.dispatch_table import fixed_launch
@@ -165,5 +165,5 @@ def test_dispatch_table_matches_sweeps():
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert fixed_launch("verify", 1500, 1500) == ("xwalk_kernel", 89)
-    assert fixed_launch("emit", 1500, 1500) == ("xwalk_kernel", 57)
+    assert fixed_launch("emit", 1500, 1500) == ("xwalk_kernel", 101)
     assert fixed_launch("verify", 1000, 1000) == ("csum_kernel", 5)

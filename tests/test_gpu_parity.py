@@ -743,6 +743,8 @@ WIDE_KERNELS = {
     46: ("xwalk_kernel", 16257),
     47: ("xwalk_kernel", 16257),
     57: ("xwalk_kernel", 16257),
+    101: ("xwalk_kernel", 16257),  # 57 with write-through segment stores (late round 6)
+    100: ("xwalk_kernel", 16257),
     80: ("xwalk_kernel", 16257),  # staged emit: field entries, then the segment pass (round 6)
     81: ("xwalk_kernel", 16257),
     48: ("xwalk_kernel", 16257),

@@ -15,7 +15,9 @@ Every variant's verify statuses and emitted bytes are checked equal to the walk 
 of the buffer), so a faster kernel that computes something else fails the sweep.
 One JSON line per (length, stride): the best of ROUNDS passes per kernel, in ms.
 PROFILE=v6mix: C4's IPv6 TCP / UDP / ICMPv6 mix instead of IPv4/UDP (one field per record).
-Usage: [KS=0-124] [ROUNDS=3] [K=12] [FORMS=aligned,unaligned,gapped] [PROFILE=udp4|v6mix]
+Late round 6: VERIFY / EMIT (comma lists) replace the variant sets, e.g. EMIT=39,47,57,101 VERIFY=5 for
+the emit table with the write-through segment form (101).
+Usage: [KS=0-124] [ROUNDS=3] [K=12] [FORMS=aligned,unaligned,gapped] [PROFILE=udp4|v6mix] [VERIFY=..] [EMIT=..]
        SMOLCSUM_LIB=.../libsmolcsum_exp.so python tools/sweep_dispatch.py > profiles/r06_dispatch_sweep_<box>.jsonl"""
 import json
 import os
@@ -29,8 +31,8 @@ import torch  # noqa: E402
 
 from smoltcp_amd import engine as E  # noqa: E402
 
-VERIFY = (5, 47, 89)
-EMIT = (39, 47, 57)
+VERIFY = tuple(int(v) for v in os.environ.get("VERIFY", "5,47,89").split(","))
+EMIT = tuple(int(v) for v in os.environ.get("EMIT", "39,47,57").split(","))
 
 
 def ks():
