@@ -209,7 +209,7 @@ bool variant_built(int v) {
         default: break;
     }
 #ifdef SMOL_EXP
-    if ((v >= 80 && v <= 96 && v != 89) || (v >= 98 && v <= 100)) return true;
+    if ((v >= 80 && v <= 96 && v != 89) || (v >= 98 && v <= 100) || v == 102) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -265,7 +265,7 @@ struct Pick {
 // Variants that serve copy-emit only: copy_kernel (17, 21; 22 / 30 experiments), the transposed
 // layout (49-55, experiments) and the walk kernel's MODE_COPY forms 8 / 11 / 16 (experiments).  Forced
 // on a context, they leave emit / verify / data to the library's choice (the automatic dispatch).
-bool copy_only(int v) { return v == 8 || v == 11 || v == 16 || v == 17 || v == 21 || v == 22 || v == 30 || v == 98 || (v >= 49 && v <= 55); }
+bool copy_only(int v) { return v == 8 || v == 11 || v == 16 || v == 17 || v == 21 || v == 22 || v == 30 || v == 98 || v == 102 || (v >= 49 && v <= 55); }
 
 Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* b, const KParams& p) {
     const bool has_desc = b->desc != nullptr;
@@ -277,8 +277,8 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
         // (21; tools/exp_copy.py, MI355X).  Variants 1 / 8 / 11 / 16 / 17 stay selectable.
         const int cv = ctx->variant;
         if (cv >= 49 && cv <= 55 && xcopy_fits(p)) return {F_XCOPY, cv, -1};
-        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17 || cv == 22 || cv == 30 || cv == 98) ? cv : 21;
-        const bool ck = var == 17 || var == 21 || var == 22 || var == 30 || var == 98;
+        const int var = (cv == 1 || cv == 8 || cv == 11 || cv == 16 || cv == 17 || cv == 22 || cv == 30 || cv == 98 || cv == 102) ? cv : 21;
+        const bool ck = var == 17 || var == 21 || var == 22 || var == 30 || var == 98 || var == 102;
         const int gv = cv >= 0 ? cv : walk_variant(mode, has_desc);
         const int shape = ctx->shape >= 0 ? ctx->shape : ck ? (int)CFG_G16U4 : auto_shape(b->len, has_desc, line_grid(gv), gv);
         return {ck ? F_COPY : F_WALK, var, shape};

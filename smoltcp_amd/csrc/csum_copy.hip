@@ -74,7 +74,8 @@ constexpr int NOF = -(1 << 20);  // "no field" for store_part
 // NTB (experiments build): bit 0 the body chunks stored non-temporal (variant 30), bit 1 also the
 // body's source chunks loaded non-temporal (variant 22); bit 2 the destination chunks of the generic
 // (header / edge) chunks loaded non-temporal (variant 98, round 6: whether the 28-B header reads
-// then leave L2 as 64-B requests instead of whole 128-B lines).
+// then leave L2 as 64-B requests instead of whole 128-B lines; they do not); bit 3 the body chunks
+// stored write-through non-temporal, sc1 nt (variant 102, round 6; cf. variant 30's plain nt).
 template <int G, int U, bool IMPLICIT, int UW0 = 0, int UB = 0, bool LBS = false, int NTB = 0>
 __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
     using namespace copy2;
@@ -285,7 +286,9 @@ __global__ __launch_bounds__(256) void copy_kernel(KParams p) {
             acc = sum_chunk(m, pos, s1, acc);
             const gu8 dst = (gu8)base + 16u * k;
             if (!far) {
-                if constexpr ((NTB & 1) != 0) __builtin_nontemporal_store(m, (GMEM u32x4*)dst);
+                if constexpr ((NTB & 8) != 0)  // (variant 102) write-through non-temporal vector store
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(dst), "v"(m) : "memory");
+                else if constexpr ((NTB & 1) != 0) __builtin_nontemporal_store(m, (GMEM u32x4*)dst);
                 else *(GMEM u32x4*)dst = m;
             } else store_part(dst, m, 0, 16, f0b - pos, f1b - pos, f2b - pos);
         };
@@ -322,7 +325,7 @@ hipError_t launch_copy2_one(const KParams& p, uint32_t max_blocks, hipStream_t s
     constexpr uint32_t GPB = 256 / G;
     const uint64_t want = (p.n + GPB - 1) / GPB;
     const uint32_t blocks = grid_blocks(want, max_blocks);
-    note_launch(KERN_COPY, NTB == 1 ? 30 : NTB == 3 ? 22 : NTB == 4 ? 98 : LBS ? 21 : 17, G, U);
+    note_launch(KERN_COPY, NTB == 1 ? 30 : NTB == 3 ? 22 : NTB == 4 ? 98 : NTB == 8 ? 102 : LBS ? 21 : 17, G, U);
     hipLaunchKernelGGL((copy_kernel<G, U, IMPLICIT, UW, UB, LBS, NTB>), dim3(blocks), dim3(256), 0, s, p);
     return hipGetLastError();
 }
@@ -379,6 +382,9 @@ hipError_t launch_copy_nt(int var, const KParams& p, uint32_t max_blocks, hipStr
     if (var == 98)
         return im ? launch_copy2_one<true, 16, 4, 1, 2, true, 4>(p, max_blocks, s)
                   : launch_copy2_one<false, 16, 4, 1, 2, true, 4>(p, max_blocks, s);
+    if (var == 102)
+        return im ? launch_copy2_one<true, 16, 4, 1, 2, true, 8>(p, max_blocks, s)
+                  : launch_copy2_one<false, 16, 4, 1, 2, true, 8>(p, max_blocks, s);
     return im ? launch_copy2_one<true, 16, 4, 1, 2, true, 3>(p, max_blocks, s)
               : launch_copy2_one<false, 16, 4, 1, 2, true, 3>(p, max_blocks, s);
 }

@@ -78,7 +78,8 @@ struct VarT {
     static constexpr bool BSEG6 = VAR == 38 || VAR == 39 || VAR == 40 || VAR == 12 || VAR == 14;
     static constexpr bool BSEG_NO4 = VAR == 39 || VAR == 40 || VAR == 12 || VAR == 14;
     static constexpr int CU0 = VAR == 12 ? 2 : 0;
-    // 40 (experiments build): 39 with the whole segments stored non-temporal
+    // 40 (experiments build): 39 with the whole segments stored non-temporal (round 5: plain nt, lost;
+    // since late round 6 write-through, sc1 nt, as the transposed walk's variant 101)
     static constexpr bool NTSEG = VAR == 40;
     static constexpr bool NOSHARE = VAR == 31 || VAR == 32 || VAR == 34 || VAR == 35;
     static constexpr int BASE = (VAR == 31 || VAR == 35 || VAR == 36 || VAR == 37 || VAR == 38) ? 5
@@ -1130,7 +1131,8 @@ __device__ __forceinline__ bool walk_step(const KParams& p, Walk& w, Regs<U, MOD
                     auto seg_store = [&](uint64_t d) {
                         const u32x2 x = *reinterpret_cast<const u32x2*>(winb + (d - base));
                         if constexpr (NOSTORE) asm volatile("" ::"v"(x), "v"(d));
-                        else if constexpr (VarT<VAR>::NTSEG) __builtin_nontemporal_store(x, (GMEM u32x2*)d);
+                        else if constexpr (VarT<VAR>::NTSEG)  // write-through non-temporal vector store
+                            asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(d), "v"(x) : "memory");
                         else *(GMEM u32x2*)d = x;
                     };
                     if (wsA != ~0ull && lane < 8) seg_store(wsA + 8u * (uint32_t)lane);
@@ -1467,6 +1469,7 @@ hipError_t launch_copy(int shape, int var, const KParams& p, uint32_t max_blocks
 #ifdef SMOL_EXP
         case 30:
         case 98:
+        case 102:
         case 22: return launch_copy_nt(var, p, max_blocks, s);
         case 1: return launch_copy_var<IMPLICIT, 1>(shape, p, max_blocks, s);
         case 11: return launch_copy_var<IMPLICIT, 11>(shape, p, max_blocks, s);

@@ -481,7 +481,8 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         return;
     }
 #ifdef SMOL_EXP
-    if (variant >= 64) {
+    // 64 + 44 / 64 + 47: stores compiled out (timing only); the numbers from 80 up are round-6 forms
+    if (variant == 64 + 44 || variant == 64 + 47) {
         if (seg) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, true, true>), dim3(blocks), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, true, false>), dim3(blocks), dim3(256), 0, s, p);
         return;

@@ -119,7 +119,7 @@ def _run(eng, recs, copies_spec, caps=(0, 0, 0, 0, 0), shape=-1, fixed_stride=No
         eng.set_max_blocks(0)
     if n:  # the forced variant ran its own kernel (default: copy_kernel variant 21)
         want = ("csum_kernel", variant) if variant in (1, 8, 11, 16) else \
-            ("copy_kernel", variant if variant in (17, 22, 30) else 21)
+            ("copy_kernel", variant if variant in (17, 22, 30, 98, 102) else 21)
         if variant in (49, 50, 55) and fixed_stride and 1024 <= (fixed_len or fixed_stride) <= 1921:
             want = ("copy_kernel", variant)  # the transposed layout (csum_xcopy.hip)
         assert (launched["kernel"], launched["variant"]) == want, (variant, launched)
@@ -186,7 +186,7 @@ def test_copy_emit_fixed_stride_mixed(eng, stride, length):
         # the default (17), a capped grid, the prefetch variant (1), the two-load variant (8), the
         # lane-shuffle variants (11, 16)
         for variant, blocks in ((-1, 0), (-1, 7), (1, 0), (11, 0), (11, 7), (8, 0), (8, 7), (16, 0), (16, 7), (17, 0),
-                               (17, 7), (21, 0), (21, 7), (49, 0), (50, 0)):
+                               (17, 7), (21, 0), (21, 7), (49, 0), (50, 0), (98, 0), (102, 0), (102, 7)):
             if not eng.has(variant):
                 continue
             _run(eng, recs, spec, fixed_stride=stride, fixed_len=length, variant=variant, blocks=blocks,

@@ -617,7 +617,8 @@ def test_emit_variants_match_oracle(eng, profile, kind):
                     (29, -1, 0, (0, 0, 0, 0, 0)), (29, 7, 3, (3, 2, 2, 3, 3)),
                     (37, -1, 0, (0, 0, 0, 0, 0)), (37, 7, 3, (3, 2, 2, 3, 3)), (37, 0, 0, (2, 3, 0, 1, 0)),
                     (38, -1, 0, (0, 0, 0, 0, 0)), (38, 0, 5, (0, 0, 0, 0, 0)),
-                    (39, -1, 0, (0, 0, 0, 0, 0)), (39, 7, 3, (3, 2, 2, 3, 3)), (39, 0, 5, (2, 3, 0, 1, 0))]:
+                    (39, -1, 0, (0, 0, 0, 0, 0)), (39, 7, 3, (3, 2, 2, 3, 3)), (39, 0, 5, (2, 3, 0, 1, 0)),
+                    (40, -1, 0, (0, 0, 0, 0, 0)), (40, 7, 3, (3, 2, 2, 3, 3))]:
                 if not eng.has(variant):
                     continue
                 _emit_case(eng, host, off, n, stride, L, kind, caps, variant, shape, blocks)
