@@ -150,9 +150,10 @@ int auto_variant(int mode, bool has_desc) {
 // (profiles/r06_dispatch_sweep_box{1,2,3}.jsonl), turned into dispatch_table.inc by
 // tools/gen_dispatch_table.py (the least summed time per entry).  Verify: the walk kernel (5), the
 // transposed walk (47) or 47 with the first-load hint (89: lanes 0-3 of each record's first instruction
-// with the default cache policy; C2 verify 0.2342 -> 0.2259 ms); emit: the walk kernel (39), 47 or, where
-// the sweep measured 57 (47 with non-temporal field segments) fastest, 101 (57's segments stored
-// write-through: C2 / C4 emit 1-1.7 % below 57, late round 6).  Outside 1024 .. 9023 B the walk kernel
+// with the default cache policy; C2 verify 0.2342 -> 0.2259 ms); emit: the walk kernel (39), 47, 57 (47
+// with non-temporal field segments) or 101 (57's segments stored write-through), from a second emit
+// sweep that ran all four (late round 6, profiles/r06_dispatch_sweep_wt_*.jsonl: two IPv4 boxes, two
+// IPv6-mix boxes; C2's and C4's rows take 101).  Outside 1024 .. 9023 B the walk kernel
 // (round 5: past 9000 B the two trade places by length, within 2 %).
 // Returns the transposed-walk variant to run (0: the walk kernel).
 #include "dispatch_table.inc"
@@ -164,7 +165,7 @@ int xwalk_auto(int mode, const smol_csum_batch_t* b) {
     const int col = b->stride != b->len ? 2 : (b->len % 64 == 0 ? 0 : 1);
     const char c = (mode == MODE_VERIFY ? kVerifyTable : kEmitTable)[k][col];
     if (mode == MODE_VERIFY) return c == 'h' ? 89 : c == 'x' ? 47 : 0;
-    return c == 'n' ? 101 : c == 'x' ? 47 : 0;
+    return c == 't' ? 101 : c == 'n' ? 57 : c == 'x' ? 47 : 0;
 }
 
 // The XCD block order (csum_launch.h xcd_block / xcd_chunk) when none is forced: the contiguous order

@@ -31,7 +31,7 @@ def fixed_variant(op: str, length: int, stride: int) -> int:
     c = TABLES["kVerifyTable" if op == "verify" else "kEmitTable"][k][col]
     if op == "verify":
         return {"h": 89, "x": 47, "w": 0}[c]
-    return {"n": 101, "x": 47, "w": 0}[c]
+    return {"t": 101, "n": 57, "x": 47, "w": 0}[c]
 
 
 def fixed_launch(op: str, length: int, stride: int):
