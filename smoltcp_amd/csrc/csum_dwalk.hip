@@ -99,6 +99,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160
                               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(end >> 32), (int)cnt - 1) << 32);
         stage_wave = __ballot(gap) == 0 && last - first >= (uint64_t)cnt * dwalk::kStageMinBytes;
     }
+    // LITE: the record before the wavefront's first one ends where it begins (the batch's record r - 1,
+    // loaded with the descriptors), so that record 0's field segment may start in it (below)
+    bool prev_contig = false;
+    if constexpr (LITE && (SEGF & 256) != 0) {
+        if (rw0 > 0) {
+            uint64_t pend;
+            if (p.desc) {
+                const u32x4 pd = *(gcv4)((uint64_t)p.desc + 16 * (rw0 - 1));
+                pend = pd.z >= 64 ? ((uint64_t)pd.x | ((uint64_t)pd.y << 32)) + pd.z : ~0ull;  // (>= 64 B: as ok_tail)
+            } else {
+                pend = p.len >= 64 ? (rw0 - 1) * p.stride + p.len : ~0ull;
+            }
+            const uint64_t off0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)d.x) |
+                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)d.y) << 32);
+            prev_contig = __builtin_amdgcn_readfirstlane((int)(pend == off0)) != 0;
+        }
+    }
     // wave-uniform record extents
     uint64_t A[R];
     uint32_t L[R];
@@ -181,7 +198,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160
                 flo = f[j] < flo ? f[j] : flo;
                 fhi = f[j] + 2 > fhi ? f[j] + 2 : fhi;
             }
-        const bool ok_tail = mine && (fhi == 0 || fhi + 64 <= len);
+        const bool ok_tail = mine && len >= 64 && (fhi == 0 || fhi + 64 <= len);  // (len: a segment that
+        // starts before the next record then holds only bytes of this one)
         const uint64_t okm = __ballot(lane == 0 && ok_tail);
         if (mine && (g.fam == 4 || g.fam == 6) && fhi != 0 && ok_tail) {
             const bool prev_ok = contig && gw != 0 && ((okm >> (uint32_t)(G * (gw - 1))) & 1ull);
@@ -318,10 +336,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160
                     flo = f[j] < flo ? f[j] : flo;
                     fhi = f[j] + 2 > fhi ? f[j] + 2 : fhi;
                 }
-            const bool ok_tail = mine && (fhi == 0 || fhi + 64 <= len);
+            const bool ok_tail = mine && len >= 64 && (fhi == 0 || fhi + 64 <= len);  // (len: a segment that
+            // starts before the next record then holds only bytes of this one)
             const uint64_t okm = __ballot(lane == 0 && ok_tail);
             if (mine && (g.fam == 4 || g.fam == 6) && fhi != 0 && ok_tail && f[2] == NO_FIELD) {
-                const bool prev_ok = gw != 0 && ((okm >> (uint32_t)(G * (gw - 1))) & 1ull);
+                // a segment that starts before the record holds only bytes of the record before it: in the
+                // wavefront, that record passed ok_tail; for the wavefront's first record (late round 6) it
+                // only has to end where this one begins, since a staged record's field segments end at
+                // least 64 B before its end (ok_tail) and an unstaged one's 2-B fields are written in this
+                // launch, before the segment pass loads the segment
+                const bool prev_ok = gw != 0 ? ((okm >> (uint32_t)(G * (gw - 1))) & 1ull) != 0 : prev_contig;
                 const int32_t ph = (int32_t)(a0 & 63u);
                 const int32_t rA = ((ph + (int32_t)flo) & ~63) - ph, rB = ((ph + (int32_t)fhi - 1) & ~63) - ph;
                 const int32_t wend = 16 * WIN_CH - (int32_t)hd;
@@ -423,14 +447,18 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         !(variant == 96 && mode == MODE_EMIT) && !(variant == 97 && mode == MODE_EMIT))
         return hipErrorInvalidValue;
 #endif
-    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97) && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
+    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97 || variant == 103) && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
         if (!p.stage || !p.stage_flags || p.n > kStageChunk) return hipErrorInvalidValue;
         note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
         const uint32_t b = grid_blocks((p.n + dwalk::GPB - 1) / dwalk::GPB, kMaxGridBlocks);
         if (variant == 96)  // held to 8 wavefronts per SIMD (12 B of spills per lane; 97: 7, none)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 128>), dim3(b), dim3(256), 0, s, p);
-        else if (variant == 97)
+        else if (variant == 97)  // (bit 256, late round 6: the wavefront's first record may stage too)
+            hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 256>), dim3(b), dim3(256), 0, s, p);
+#ifdef SMOL_EXP
+        else if (variant == 103)  // 97 before bit 256 (experiments build)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64>), dim3(b), dim3(256), 0, s, p);
+#endif
         else if (variant == 95)  // (experiments: held to 8 wavefronts per SIMD, 64 B of spills per lane)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27 | 32>), dim3(b), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27>), dim3(b), dim3(256), 0, s, p);

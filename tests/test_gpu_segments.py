@@ -234,7 +234,7 @@ def test_emit_write_set_concurrent(eng, gap, L):
     K = 120
     for variant, batch in ((19, fixed), (29, fixed), (-1, fixed), (23, fixed), (26, desc_batch), (28, desc_batch),
                            (-1, desc_batch), (37, fixed), (39, fixed), (44, fixed), (47, fixed), (12, fixed),
-                           (61, desc_batch), (62, desc_batch)):
+                           (61, desc_batch), (62, desc_batch), (97, desc_batch), (103, desc_batch), (101, fixed)):
         if not eng.has(variant):
             continue
         d = torch.from_numpy(host0.copy()).cuda()
@@ -301,3 +301,58 @@ def test_field_stores_flag(eng):
         # transposed walk's 44)
         kern, _ = fixed_launch("emit", L, L)
         assert (ll["kernel"], ll["variant"]) == ((kern, 44) if kern == "xwalk_kernel" else (kern, 5)), (L, ll)
+
+
+def test_staged_emit_tiny_neighbours_concurrent(eng):
+    """The staged descriptor emit (97, and 103 / 94 from the experiments build) next to records that
+    give its shared-segment rule trouble: long IPv4/TCP records back to back with tiny raw records
+    (12-60 B, no fields) before them, and small gaps before some wavefronts' first records.  While
+    emit runs, another stream rewrites every byte outside the records; those bytes must end with that
+    stream's last value and the records must equal the oracle's emit (a segment may start in the
+    record before only when that record is at least 64 B long and ends where this one begins)."""
+    rng = np.random.default_rng(0x71)
+    n = 8192
+    lens = rng.integers(1100, 2400, n).astype(np.uint32)
+    tiny = rng.random(n) < 0.2
+    lens[tiny] = rng.integers(12, 61, int(tiny.sum()))
+    gaps = np.where(rng.random(n) < 0.1, rng.integers(1, 40, n), 0).astype(np.uint64)
+    pre, post = 4096, 4096
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[1:])
+    total = pre + int(offs[-1] + lens[-1]) + post
+    buf = torch.zeros(total, dtype=torch.uint8, device="cuda:0")
+    batch = E.Batch.from_records(offs, lens, E.KIND_IP, "cuda:0")
+    eng.synth(buf[pre:], batch, E.SYNTH_TCP4, seed=0x71)
+    host0 = buf.cpu().numpy().copy()
+    for j in np.nonzero(tiny)[0]:  # raw junk: no IP header the parse accepts
+        a = pre + int(offs[j])
+        host0[a: a + int(lens[j])] = 0
+    inside = np.zeros(total, dtype=bool)
+    for o, l in zip(offs, lens):
+        inside[pre + int(o): pre + int(o) + int(l)] = True
+    outside_idx = torch.from_numpy(np.nonzero(~inside)[0]).cuda()
+    ref = host0[pre:].copy()
+    oracle.batch_emit(ref, P.oracle_desc(offs, lens, E.KIND_IP), n, 0, 0, E.KIND_IP)
+    s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
+    K = 60
+    ran = 0
+    for variant in (-1, 97, 103, 94):
+        if not eng.has(variant):
+            continue
+        ran += 1
+        d = torch.from_numpy(host0.copy()).cuda()
+        torch.cuda.synchronize()
+        eng.set_variant(variant)
+        try:
+            for k in range(1, K + 1):
+                with torch.cuda.stream(s_write):
+                    d.index_fill_(0, outside_idx, k)
+                if k % 6 == 1:
+                    eng.emit(d[pre:], batch, stream=s_emit)
+            torch.cuda.synchronize()
+        finally:
+            eng.set_variant(-1)
+        got = d.cpu().numpy()
+        assert (got[~inside] == K).all(), (variant, np.nonzero(got[~inside] != K)[0][:8])
+        assert np.array_equal(got[pre:][inside[pre:]], ref[inside[pre:]]), variant
+    assert ran >= 2
