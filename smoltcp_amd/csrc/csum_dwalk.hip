@@ -86,6 +86,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160
     constexpr bool LITE = (SEGF & 64) != 0 && MODE == MODE_EMIT;
     constexpr bool STAGE_ANY = (SEGF & 16) != 0 || LITE;
     bool stage_wave = false;
+    // GAPS (bit 512, LITE, late round 6): a wavefront stages whatever its records' layout (gaps,
+    // shuffled descriptors) when their mean length is >= kStageMinBytes; each record's segment may
+    // start in the record before it only when that one (the batch's record r - 1) ends where it begins
+    constexpr bool GAPS = (SEGF & 512) != 0 && (SEGF & 64) != 0 && MODE == MODE_EMIT;
+    uint64_t cmask = ~0ull;  // GAPS: lane j set when record j - 1 of the wavefront ends where j begins (>= 64 B)
     if constexpr (STAGE_ANY) {
         // from the descriptors in lanes 0 .. cnt - 1 (not the uniform arrays: they would stay live
         // in SGPRs, 87 against 58, one wavefront per SIMD fewer): back to back, and their span
@@ -97,7 +102,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160
                                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)d.y) << 32);
         const uint64_t last = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)end, (int)cnt - 1) |
                               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(end >> 32), (int)cnt - 1) << 32);
-        stage_wave = __ballot(gap) == 0 && last - first >= (uint64_t)cnt * dwalk::kStageMinBytes;
+        if constexpr (GAPS) {
+            uint32_t lz = (uint32_t)wl < cnt ? d.z : 0u;
+#pragma unroll
+            for (int m = 1; m < R; m <<= 1) lz += (uint32_t)__shfl_xor((int)lz, m, 64);
+            const uint32_t plen = (uint32_t)__shfl_up((int)d.z, 1, 64);
+            cmask = __ballot((uint32_t)wl < cnt && wl != 0 && pend == off && plen >= 64u);
+            stage_wave = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)lz) >= (uint64_t)cnt * dwalk::kStageMinBytes;
+        } else {
+            stage_wave = __ballot(gap) == 0 && last - first >= (uint64_t)cnt * dwalk::kStageMinBytes;
+        }
     }
     // LITE: the record before the wavefront's first one ends where it begins (the batch's record r - 1,
     // loaded with the descriptors), so that record 0's field segment may start in it (below)
@@ -345,7 +359,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160
                 // only has to end where this one begins, since a staged record's field segments end at
                 // least 64 B before its end (ok_tail) and an unstaged one's 2-B fields are written in this
                 // launch, before the segment pass loads the segment
-                const bool prev_ok = gw != 0 ? ((okm >> (uint32_t)(G * (gw - 1))) & 1ull) != 0 : prev_contig;
+                const bool prev_ok = gw != 0 ? (((okm >> (uint32_t)(G * (gw - 1))) & 1ull) != 0 && ((cmask >> gw) & 1ull) != 0)
+                                             : prev_contig;
                 const int32_t ph = (int32_t)(a0 & 63u);
                 const int32_t rA = ((ph + (int32_t)flo) & ~63) - ph, rB = ((ph + (int32_t)fhi - 1) & ~63) - ph;
                 const int32_t wend = 16 * WIN_CH - (int32_t)hd;
@@ -447,7 +462,7 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         !(variant == 96 && mode == MODE_EMIT) && !(variant == 97 && mode == MODE_EMIT))
         return hipErrorInvalidValue;
 #endif
-    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97 || variant == 103) && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
+    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97 || variant == 103 || variant == 104) && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
         if (!p.stage || !p.stage_flags || p.n > kStageChunk) return hipErrorInvalidValue;
         note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
         const uint32_t b = grid_blocks((p.n + dwalk::GPB - 1) / dwalk::GPB, kMaxGridBlocks);
@@ -456,6 +471,8 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         else if (variant == 97)  // (bit 256, late round 6: the wavefront's first record may stage too)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 256>), dim3(b), dim3(256), 0, s, p);
 #ifdef SMOL_EXP
+        else if (variant == 104)  // 97 + bit 512 (experiments build): staging over gapped / shuffled layouts
+            hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 256 | 512>), dim3(b), dim3(256), 0, s, p);
         else if (variant == 103)  // 97 before bit 256 (experiments build)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64>), dim3(b), dim3(256), 0, s, p);
 #endif

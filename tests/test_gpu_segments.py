@@ -234,7 +234,7 @@ def test_emit_write_set_concurrent(eng, gap, L):
     K = 120
     for variant, batch in ((19, fixed), (29, fixed), (-1, fixed), (23, fixed), (26, desc_batch), (28, desc_batch),
                            (-1, desc_batch), (37, fixed), (39, fixed), (44, fixed), (47, fixed), (12, fixed),
-                           (61, desc_batch), (62, desc_batch), (97, desc_batch), (103, desc_batch), (101, fixed)):
+                           (61, desc_batch), (62, desc_batch), (97, desc_batch), (103, desc_batch), (104, desc_batch), (101, fixed)):
         if not eng.has(variant):
             continue
         d = torch.from_numpy(host0.copy()).cuda()
@@ -336,7 +336,7 @@ def test_staged_emit_tiny_neighbours_concurrent(eng):
     s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
     K = 60
     ran = 0
-    for variant in (-1, 97, 103, 94):
+    for variant in (-1, 97, 103, 104, 94):
         if not eng.has(variant):
             continue
         ran += 1
