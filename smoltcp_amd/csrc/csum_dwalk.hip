@@ -419,6 +419,8 @@ __device__ __forceinline__ uint64_t patch_field(uint64_t x, int64_t k, uint32_t 
     return x;
 }
 
+#ifdef SMOL_EXP
+// (experiments build, variant 105: the first form, 8 lanes x 8 B per record, 1024-thread workgroups)
 __global__ __launch_bounds__(1024) void seg_pass_kernel(KParams p) {
     const uint64_t r = (uint64_t)blockIdx.x * 128 + (threadIdx.x >> 3);
     const int l = (int)(threadIdx.x & 7);
@@ -446,11 +448,58 @@ __global__ __launch_bounds__(1024) void seg_pass_kernel(KParams p) {
         asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(wB), "v"(xb) : "memory");
     }
 }
+#endif
 
-hipError_t launch_seg_pass(const KParams& p, hipStream_t s) {
-    // 1024-thread workgroups (128 records each): a chunk whose wavefronts mostly find nothing staged
-    // costs the dispatch of a quarter as many workgroups
-    hipLaunchKernelGGL(seg_pass_kernel, dim3((uint32_t)((p.n + 127) / 128)), dim3(1024), 0, s, p);
+// 4 lanes per record, 16 B each (late round 6: one 16-B load and one 16-B store per lane and segment
+// instead of two 8-B ones, 256-thread workgroups: C3 emit 0.791 -> 0.777 ms, interleaved bench lines,
+// profiles/r06_experiments/seg_pass_16b_lanes.txt)
+__global__ __launch_bounds__(256) void seg_pass4_kernel(KParams p) {
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    const uint64_t r = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+    const int l = (int)(threadIdx.x & 3);
+    if (r >= p.n) return;
+    if (p.stage_flags[r / 8] == 0u) return;
+    const uint64_t e = __builtin_nontemporal_load((const GMEM uint64_t*)(p.stage + r));
+    if (e == ~0ull) return;
+    const uint64_t off = p.desc ? *(const GMEM uint64_t*)((uint64_t)p.desc + 16 * r) : r * p.stride;
+    const uint32_t f0 = (uint32_t)(e & 0xffu), f1 = (uint32_t)((e >> 8) & 0xffu);
+    const uint32_t v0 = (uint32_t)((e >> 32) & 0xffffu), v1 = (uint32_t)(e >> 48);
+    const uint64_t a0 = (uint64_t)p.buf + off;
+    const uint32_t lo = min(f0 == 0xffu ? 0xffffu : f0, f1 == 0xffu ? 0xffffu : f1);
+    const uint32_t hi = max(f0 == 0xffu ? 0u : f0 + 2, f1 == 0xffu ? 0u : f1 + 2);
+    const uint64_t sA = (a0 + lo) & ~63ull, sB = (a0 + hi - 1) & ~63ull;
+    const uint64_t wA = sA + 16u * (uint32_t)l, wB = sB + 16u * (uint32_t)l;
+    u32x4v xa = *(const GMEM u32x4v*)wA;
+    u32x4v xb = sB != sA ? *(const GMEM u32x4v*)wB : u32x4v{0, 0, 0, 0};
+    auto patch = [&](u32x4v& x, uint64_t w) {
+        uint64_t q0 = (uint64_t)x.x | ((uint64_t)x.y << 32), q1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+        if (f0 != 0xffu) {
+            q0 = patch_field(q0, (int64_t)(a0 + f0) - (int64_t)w, v0);
+            q1 = patch_field(q1, (int64_t)(a0 + f0) - (int64_t)(w + 8), v0);
+        }
+        if (f1 != 0xffu) {
+            q0 = patch_field(q0, (int64_t)(a0 + f1) - (int64_t)w, v1);
+            q1 = patch_field(q1, (int64_t)(a0 + f1) - (int64_t)(w + 8), v1);
+        }
+        x = u32x4v{(uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32)};
+    };
+    patch(xa, wA);
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(wA), "v"(xa) : "memory");
+    if (sB != sA) {
+        patch(xb, wB);
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(wB), "v"(xb) : "memory");
+    }
+}
+
+hipError_t launch_seg_pass(const KParams& p, hipStream_t s, int form) {
+#ifdef SMOL_EXP
+    if (form == 1) {  // the first form: 1024-thread workgroups (128 records each)
+        hipLaunchKernelGGL(seg_pass_kernel, dim3((uint32_t)((p.n + 127) / 128)), dim3(1024), 0, s, p);
+        return hipGetLastError();
+    }
+#endif
+    (void)form;
+    hipLaunchKernelGGL(seg_pass4_kernel, dim3((uint32_t)((p.n + 63) / 64)), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -462,13 +511,14 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         !(variant == 96 && mode == MODE_EMIT) && !(variant == 97 && mode == MODE_EMIT))
         return hipErrorInvalidValue;
 #endif
-    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97 || variant == 103 || variant == 104) && mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
+    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97 || variant == 103 || variant == 104 || variant == 105) &&
+        mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
         if (!p.stage || !p.stage_flags || p.n > kStageChunk) return hipErrorInvalidValue;
         note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
         const uint32_t b = grid_blocks((p.n + dwalk::GPB - 1) / dwalk::GPB, kMaxGridBlocks);
         if (variant == 96)  // held to 8 wavefronts per SIMD (12 B of spills per lane; 97: 7, none)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 128>), dim3(b), dim3(256), 0, s, p);
-        else if (variant == 97)  // (bit 256, late round 6: the wavefront's first record may stage too)
+        else if (variant == 97 || variant == 105)  // (bit 256, late round 6: the wavefront's first record may stage too; 105: the first segment-pass form)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 256>), dim3(b), dim3(256), 0, s, p);
 #ifdef SMOL_EXP
         else if (variant == 104)  // 97 + bit 512 (experiments build): staging over gapped / shuffled layouts
@@ -481,7 +531,7 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         else hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 27>), dim3(b), dim3(256), 0, s, p);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        return launch_seg_pass(p, s);
+        return launch_seg_pass(p, s, variant == 105 ? 1 : 0);
     }
     const uint64_t per = (uint64_t)dwalk::GPB;
     note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);

@@ -93,7 +93,7 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // STAGE (variants 80 / 81, round 6; emit): the field segments are not written here.  A record whose
 // fields the whole segments cover (47's rule, all or nothing) stages one 8-B entry (its two field
 // offsets and values, csum_walk.h stage_entry) in p.stage, and the segment pass (csum_dwalk.hip
-// seg_pass_kernel) writes the segments after this launch; any other
+// seg_pass4_kernel) writes the segments after this launch; any other
 // record writes its fields here as 2-B stores and stages nothing.  NTS = 32 (variant 80): the
 // lanes of a record's first instruction that hold the segments of record offsets [10, 28) (an IPv4
 // record's two fields) load with the default cache policy, so that the segment pass finds those lines

@@ -336,7 +336,7 @@ def test_staged_emit_tiny_neighbours_concurrent(eng):
     s_emit, s_write = torch.cuda.Stream(), torch.cuda.Stream()
     K = 60
     ran = 0
-    for variant in (-1, 97, 103, 104, 94):
+    for variant in (-1, 97, 103, 104, 105, 94):
         if not eng.has(variant):
             continue
         ran += 1

@@ -37,7 +37,7 @@ def kernel_role(name: str):
     """'emit' / 'verify' / 'data' for the checksum kernels, else None."""
     if re.search(r"copy_kernel<", name):  # csum_copy.hip: <G, U, IMPLICIT>, copy-emit only
         return "copy_emit"
-    if "seg_pass_kernel" in name:  # csum_dwalk.hip: the staged emit's second launch
+    if re.search(r"seg_pass\d*_kernel", name):  # csum_dwalk.hip: the staged emit's second launch
         return "emit_seg_pass"
     m = re.search(r"[xd]walk_kernel<([^>]*)>", name)  # csum_xwalk.hip <MODE, R, ...>, csum_dwalk.hip <MODE, ...>
     if m:
@@ -109,7 +109,7 @@ def main():
         # sum (what bench.py's HIP events around the call time), the parts stay beside it
         st, sp = cfg["emit"], cfg["emit_seg_pass"]
         cfg["emit_staging"] = st
-        cfg["emit"] = {"kernel": st["kernel"] + " + seg_pass_kernel",
+        cfg["emit"] = {"kernel": st["kernel"] + " + " + sp["kernel"],
                        **{k: st[k] + sp[k] for k in ("hbm_bytes_per_launch", "read_bytes_corrected", "write_bytes")}}
         if "kernel_trace_avg_ns" in st and "kernel_trace_avg_ns" in sp:
             cfg["emit"]["kernel_trace_avg_ns"] = st["kernel_trace_avg_ns"] + sp["kernel_trace_avg_ns"]
