@@ -650,7 +650,9 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
                   (partial ? SMOL_ST_L4_PARTIAL : 0u) | (ip_valid ? SMOL_ST_IP_VALID : 0u) |
                   (l4_valid ? SMOL_ST_L4_VALID : 0u) |
                   ((ip_ok && l4_ok && !mal) ? SMOL_ST_ACCEPT : 0u);
-            ((gu8)p.status)[r] = (uint8_t)st;
+            if constexpr (NOSTORE) asm volatile("" ::"v"(st));  // (timing only: no status byte)
+            else if constexpr (NTST) __builtin_nontemporal_store((uint8_t)st, (gu8)p.status + r);  // (verify: experiments)
+            else ((gu8)p.status)[r] = (uint8_t)st;
         }
     }
 }

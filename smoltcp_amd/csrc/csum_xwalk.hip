@@ -101,13 +101,13 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // writes that land while a read stream runs cost 65-77 ps each, the same writes in a pass of their own
 // ~20 ps.
 template <int MODE, int R, bool NOSTORE, bool SEG, bool PERSIST = false, int NTS = 0, bool HALF = false,
-          bool STAGE = false, int HINT = 0, int WPE = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void xwalk_kernel(KParams p) {
+          bool STAGE = false, int HINT = 0, int WPE = 0, int WV = xwalk::WAVES>
+__global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void xwalk_kernel(KParams p) {
     using namespace xwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
     constexpr int G = 64 / R;    // lanes per record
     constexpr int NS = 16 / R;   // load instructions (1 KiB each) per record
-    constexpr int GPB = WAVES * R;
+    constexpr int GPB = WV * R;  // WV: wavefronts per workgroup (8 in variant 107: a workgroup's 64 status bytes fill one segment)
     __shared__ u32x4 win[GPB][WIN_CH];
     __shared__ uint32_t spanbuf[GPB];
     const int wl = (int)(threadIdx.x & 63);
@@ -120,8 +120,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
     // packed records share lines with their neighbours (each line is loaded once); with a gap every
     // record loads all its lines and sums them masked to its span
     const bool packed = stride == (uint64_t)len;
-    const uint64_t nwaves = PERSIST ? (uint64_t)gridDim.x * WAVES : 0;
-    uint64_t tw = logical_block(p.xcd_remap) * WAVES + (uint64_t)wv;  // the wavefront's step
+    const uint64_t nwaves = PERSIST ? (uint64_t)gridDim.x * WV : 0;
+    uint64_t tw = logical_block(p.xcd_remap) * WV + (uint64_t)wv;  // the wavefront's step
     if (tw * R >= p.n) return;
 
     // ---- all loads of a step's records (record j: chunks below nload_j of its line grid) ----
@@ -352,8 +352,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? W
         }
     } else {
         if (mine)
-            finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE>(p, g, lane == 0 ? tot : 0u, rd, winb, hd, a0,
-                                                                         r, lane);
+            finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE, (NTS & 128) != 0>(p, g, lane == 0 ? tot : 0u, rd,
+                                                                                           winb, hd, a0, r, lane);
     }
     if (!more) break;
     wave_lds_sync();  // the windows are rewritten by the next step
@@ -382,6 +382,23 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else if (variant == 83) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if (variant == 108 && mode == MODE_VERIFY) {  // 89 with the status bytes stored non-temporal (NTS 128)
+        hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 128, false, false, 7>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if (variant == 107 && mode == MODE_VERIFY && R == 8) {  // 89 in 512-thread workgroups (64 records, 64 status bytes)
+        hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7, 0, 8>), dim3((blocks + 1) / 2),
+                           dim3(512), 0, s, p);
+        return;
+    }
+    if ((variant == 107 || variant == 108) && mode == MODE_EMIT) {  // (107's / 108's emit: 101)
+        hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 65>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if (variant == 106 && mode == MODE_VERIFY) {  // 89 without its status stores (timing only, experiments build)
+        hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, true, false, false, 0, false, false, 7>), dim3(blocks), dim3(256), 0, s, p);
         return;
     }
     if (variant == 100) {  // round 6: 57 with the segments stored sc0 sc1 nt (101: sc1 nt, the product's); verify: 89
