@@ -194,7 +194,7 @@ int field_store_variant(int variant, bool has_desc) {
     if (variant == 61) return 60;  // the descriptor walk's emit: 2-B stores (62: cached windows, 63)
     if (variant == 62 || variant == 18) return 63;  // (63 stores 2-B fields only)
     if (variant == 20) return 60;
-    if (variant == 41 || (variant >= 94 && variant <= 97) || (variant >= 103 && variant <= 105)) return 41;
+    if (variant == 41 || (variant >= 94 && variant <= 97) || (variant >= 103 && variant <= 105) || variant == 109) return 41;
     if (variant == 26 || variant == 27 || variant == 28) return 13;
     return variant;
 }
@@ -210,7 +210,7 @@ bool variant_built(int v) {
         default: break;
     }
 #ifdef SMOL_EXP
-    if ((v >= 80 && v <= 96 && v != 89) || (v >= 98 && v <= 100) || (v >= 102 && v <= 108)) return true;
+    if ((v >= 80 && v <= 96 && v != 89) || (v >= 98 && v <= 100) || (v >= 102 && v <= 109)) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -316,12 +316,12 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     // 18 / 20 (non-temporal 2-B fields) in the experiments build, which also runs them forced over
     // fixed-stride batches
     if (mode == MODE_VERIFY) {
-        if (variant == 41 || variant == 18 || variant == 62 || (variant >= 94 && variant <= 97) || (variant >= 103 && variant <= 105)) variant = 63;  // emit forms of 63
+        if (variant == 41 || variant == 18 || variant == 62 || (variant >= 94 && variant <= 97) || (variant >= 103 && variant <= 105) || variant == 109) variant = 63;  // emit forms of 63
         if (variant == 20 || variant % 64 == 61) variant = 60;              // emit forms of 60
     }
 #ifdef SMOL_EXP
     const bool dw_var = variant % 64 == 56 || variant == 60 || variant % 64 == 61 || variant == 62 || variant == 63 ||
-                        variant == 18 || variant == 20 || variant == 41 || (variant >= 94 && variant <= 97) || (variant >= 103 && variant <= 105);
+                        variant == 18 || variant == 20 || variant == 41 || (variant >= 94 && variant <= 97) || (variant >= 103 && variant <= 105) || variant == 109;
     const bool dw_ok = (mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc;
 #else
     const bool dw_var = variant == 60 || variant == 63 || variant == 41 || variant == 97;

@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((SEGF & 160
     }
     // ---- finish: the walk kernel's gates ----
     if constexpr (LITE) {
-        if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE, false, true>(p, g, a1, rd, winb, hd, a0, r, lane,
+        if (mine) finish_gates<G, MODE, false, decltype(rd), 0, false, NOSTORE, (SEGF & 1024) != 0, true>(p, g, a1, rd, winb, hd, a0, r, lane,
                                                                                             nullptr, ~0ull, ~0ull,
                                                                                             !stage_wave ? 0 : lite_staged ? 1 : 2);
         if (wl == 0) p.stage_flags[rw0 / R] = stage_wave ? 1u : 0u;
@@ -511,7 +511,7 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         !(variant == 96 && mode == MODE_EMIT) && !(variant == 97 && mode == MODE_EMIT))
         return hipErrorInvalidValue;
 #endif
-    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97 || variant == 103 || variant == 104 || variant == 105) &&
+    if ((variant == 94 || variant == 95 || variant == 96 || variant == 97 || (variant >= 103 && variant <= 105) || variant == 109) &&
         mode == MODE_EMIT) {  // staged: the staging launch, then the segment pass
         if (!p.stage || !p.stage_flags || p.n > kStageChunk) return hipErrorInvalidValue;
         note_launch(KERN_DWALK, (uint32_t)variant, dwalk::G, dwalk::U);
@@ -521,6 +521,8 @@ hipError_t launch_dwalk(int mode, int variant, const KParams& p, hipStream_t s) 
         else if (variant == 97 || variant == 105)  // (bit 256, late round 6: the wavefront's first record may stage too; 105: the first segment-pass form)
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 256>), dim3(b), dim3(256), 0, s, p);
 #ifdef SMOL_EXP
+        else if (variant == 109)  // 97 + bit 1024 (experiments build): entries (and 2-B fields) stored write-through / nt
+            hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 256 | 1024>), dim3(b), dim3(256), 0, s, p);
         else if (variant == 104)  // 97 + bit 512 (experiments build): staging over gapped / shuffled layouts
             hipLaunchKernelGGL((dwalk_kernel<MODE_EMIT, false, true, 10 | 64 | 256 | 512>), dim3(b), dim3(256), 0, s, p);
         else if (variant == 103)  // 97 before bit 256 (experiments build)

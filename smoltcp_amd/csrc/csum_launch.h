@@ -136,7 +136,7 @@ hipError_t launch_xwalk(int mode, int variant, const KParams& p, hipStream_t s);
 // the segment pass writes the field segments whole (csum_xwalk.hip).  Records per launch pair:
 constexpr uint64_t kStageChunk = 1ull << 21;
 inline bool staged_variant(int v) { return v == 80 || v == 81; }
-inline bool staged_desc_variant(int v) { return (v >= 94 && v <= 97) || (v >= 103 && v <= 105); }  // csum_dwalk.hip
+inline bool staged_desc_variant(int v) { return (v >= 94 && v <= 97) || (v >= 103 && v <= 105) || v == 109; }  // csum_dwalk.hip
 // The segment pass of the staged emit (csum_dwalk.hip seg_pass4_kernel), after the staging launch.
 hipError_t launch_seg_pass(const KParams& p, hipStream_t s, int form = 0);
 

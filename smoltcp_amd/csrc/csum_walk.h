@@ -635,7 +635,12 @@ __device__ __forceinline__ void finish_gates(const KParams& p, const Geom& g, ui
         } else if (EMITS) {
             if (STG && stg == 1) {
                 const uint64_t e = stage_entry(fip == MF_NONE ? 0xffu : fip, vip, fl4 == MF_NONE ? 0xffu : fl4, vl4);
-                __builtin_nontemporal_store(e, (GMEM uint64_t*)(p.stage + r));
+                if constexpr (NTST) {  // (experiments, dwalk variant 109) write-through non-temporal vector store
+                    const uint64_t a = (uint64_t)(p.stage + r);
+                    asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(a), "v"(e) : "memory");
+                } else {
+                    __builtin_nontemporal_store(e, (GMEM uint64_t*)(p.stage + r));
+                }
             } else {
                 if (fip != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fip, vip);
                 if (fin != MF_NONE) store_be16<NOSTORE, NTST>(wrec + fin, vin);

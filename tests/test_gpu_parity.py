@@ -282,7 +282,7 @@ def _mixed_records(rng, n=240):
     return recs
 
 
-@pytest.mark.parametrize("variant", [56, 60, 61, 62, 63, 18, 20, 41, 94, 96, 97, 103, 104, 105])
+@pytest.mark.parametrize("variant", [56, 60, 61, 62, 63, 18, 20, 41, 94, 96, 97, 103, 104, 105, 109])
 def test_dwalk_descriptor_batches(eng, variant):
     """The descriptor walks (63: the product's descriptor verify / emit, cached header windows; 60:
     non-temporal windows; experiments build: 56, and 61 / 62 = 60's / 63's emit with whole field
