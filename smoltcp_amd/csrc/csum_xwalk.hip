@@ -393,6 +393,15 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
                            dim3(512), 0, s, p);
         return;
     }
+    if ((variant == 110 || variant == 112) && mode == MODE_EMIT) {  // 101 + first-load hint 7 (110) / 1 (112); verify: 89
+        if (variant == 110) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 65, false, false, 7>), dim3(blocks), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 65, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if ((variant == 110 || variant == 112) && mode == MODE_VERIFY) {
+        hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
     if ((variant == 107 || variant == 108) && mode == MODE_EMIT) {  // (107's / 108's emit: 101)
         hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 65>), dim3(blocks), dim3(256), 0, s, p);
         return;
