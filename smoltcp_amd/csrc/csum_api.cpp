@@ -210,7 +210,7 @@ bool variant_built(int v) {
         default: break;
     }
 #ifdef SMOL_EXP
-    if ((v >= 80 && v <= 96 && v != 89) || (v >= 98 && v <= 100) || (v >= 102 && v <= 110) || v == 112) return true;
+    if ((v >= 80 && v <= 96 && v != 89) || (v >= 98 && v <= 100) || (v >= 102 && v <= 110) || v == 112 || v == 113) return true;
     const int b = v >= 64 ? v - 64 : v;
     if (v >= 64) return b == 5 || b == 29 || (b >= 31 && b <= 39) || b == 44 || b == 47 || b == 56 || b == 61;
     return (v >= 0 && v <= 4) || v == 6 || (v >= 8 && v <= 11) || v == 16 || v == 19 || (v >= 23 && v <= 29) ||
@@ -306,7 +306,7 @@ Pick pick_kernel(const smol_csum_ctx_t* ctx, int mode, const smol_csum_batch_t* 
     const bool xw_var = (variant < 64 && (variant == 44 || variant == 47 || variant == 43 || variant == 45 || variant == 46 ||
                                           variant == 15 || variant == 48 || variant == 57 || variant == 58 || variant == 59)) ||
                         (variant >= 64 && (v64 == 44 || v64 == 47)) || staged_variant(variant) || (variant >= 82 && variant <= 93) ||
-                        variant == 99 || variant == 100 || variant == 101 || variant == 106 || variant == 107 || variant == 108 || variant == 110 || variant == 112;
+                        variant == 99 || variant == 100 || variant == 101 || variant == 106 || variant == 107 || variant == 108 || variant == 110 || variant == 112 || variant == 113;
     if (xw_var) {
         if ((mode == MODE_EMIT || mode == MODE_VERIFY) && !nhc && xwalk_fits(p)) return {F_XWALK, variant, -1};
         variant = fallback;

@@ -101,7 +101,7 @@ __device__ __forceinline__ uint32_t reduce_scatter(const uint32_t* acc, int wl) 
 // writes that land while a read stream runs cost 65-77 ps each, the same writes in a pass of their own
 // ~20 ps.
 template <int MODE, int R, bool NOSTORE, bool SEG, bool PERSIST = false, int NTS = 0, bool HALF = false,
-          bool STAGE = false, int HINT = 0, int WPE = 0, int WV = xwalk::WAVES>
+          bool STAGE = false, int HINT = 0, int WPE = 0, int WV = xwalk::WAVES, int STEPS = 1>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1))) void xwalk_kernel(KParams p) {
     using namespace xwalk;
     constexpr bool EMIT = MODE == MODE_EMIT;
@@ -120,8 +120,11 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(WPE > 0
     // packed records share lines with their neighbours (each line is loaded once); with a gap every
     // record loads all its lines and sums them masked to its span
     const bool packed = stride == (uint64_t)len;
-    const uint64_t nwaves = PERSIST ? (uint64_t)gridDim.x * WV : 0;
-    uint64_t tw = logical_block(p.xcd_remap) * WV + (uint64_t)wv;  // the wavefront's step
+    // STEPS (variant 113, experiments build): a workgroup takes STEPS consecutive tiles of WV wavefronts
+    // (wavefront w: tiles w, w + WV, ...), so that its records' status bytes fill whole segments
+    const uint64_t nwaves = PERSIST ? (uint64_t)gridDim.x * WV : (uint64_t)(STEPS > 1 ? WV : 0);
+    uint64_t tw = logical_block(p.xcd_remap) * WV * STEPS + (uint64_t)wv;  // the wavefront's step
+    int step = 0;
     if (tw * R >= p.n) return;
 
     // ---- all loads of a step's records (record j: chunks below nload_j of its line grid) ----
@@ -266,7 +269,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(WPE > 0
     }
     // the next step's loads, ahead of this step's finish and stores
     const uint64_t tn = tw + nwaves;
-    const bool more = PERSIST && tn * R < p.n;
+    const bool more = (PERSIST || step + 1 < STEPS) && tn * R < p.n;
     if (more) issue(tn);
     // ---- reduce-scatter: record j's sum to group j ----
     uint32_t tot = group_sum<G>(reduce_scatter<R, 32>(acc, wl)) - hs;
@@ -358,6 +361,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(WPE > 0
     if (!more) break;
     wave_lds_sync();  // the windows are rewritten by the next step
     tw = tn;
+    ++step;
     }
 }
 
@@ -382,6 +386,16 @@ static void launch_xwalk_r(int mode, int variant, uint32_t blocks, const KParams
         if (mode == MODE_VERIFY) hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else if (variant == 83) hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 1, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
         else hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 0, false, false, 1>), dim3(blocks), dim3(256), 0, s, p);
+        return;
+    }
+    if (variant == 113 && mode == MODE_VERIFY) {  // 89 with two tiles per workgroup (64 records at R = 8)
+        hipLaunchKernelGGL((xwalk_kernel<MODE_VERIFY, R, false, false, false, 0, false, false, 7, 0, xwalk::WAVES, 2>), dim3((blocks + 1) / 2),
+                           dim3(256), 0, s, p);
+        return;
+    }
+    if (variant == 113 && mode == MODE_EMIT) {  // 101 with two tiles per workgroup
+        hipLaunchKernelGGL((xwalk_kernel<MODE_EMIT, R, false, true, false, 65, false, false, 0, 0, xwalk::WAVES, 2>), dim3((blocks + 1) / 2),
+                           dim3(256), 0, s, p);
         return;
     }
     if (variant == 108 && mode == MODE_VERIFY) {  // 89 with the status bytes stored non-temporal (NTS 128)

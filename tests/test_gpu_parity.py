@@ -746,6 +746,7 @@ WIDE_KERNELS = {
     57: ("xwalk_kernel", 16257),
     101: ("xwalk_kernel", 16257),  # 57 with write-through segment stores (late round 6)
     107: ("xwalk_kernel", 16257),  # 89 in 512-thread workgroups (verify; emit 101)
+    113: ("xwalk_kernel", 16257),  # two tiles per workgroup (89 / 101)
     100: ("xwalk_kernel", 16257),
     80: ("xwalk_kernel", 16257),  # staged emit: field entries, then the segment pass (round 6)
     81: ("xwalk_kernel", 16257),
